@@ -1,0 +1,248 @@
+"""ctypes wrapper around the CPU ORACLE (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+``cpu_baseline`` leg of bench.py, where it is the checker / the timed CPU port.
+The product package (marl-delivery_amd/marl_gpu) never imports it.
+
+See mdl_oracle.c for the reference citations of every function.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+# MAPPO/helper.py:271-279 and QMIX/helper.py:270-278, in the order
+# pickup, on_time, late, closer, wasted_pick, wasted_drop, stuck, idle, away
+MAPPO_CONSTS = (5, 200, 20, 0.02, 0, 0, -0.05, -0.05, -0.01)
+QMIX_CONSTS = (0.5, 2.0, 0.2, 0.02, -0.1, -0.1, -0.05, -0.02, -0.02)
+
+MOVE_CODES = {"S": 0, "L": 1, "R": 2, "U": 3, "D": 4}
+TRAINER_MOVES = "DLRSU"
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, i32, u32, f64, f32 = C.c_void_p, C.c_int, C.c_uint32, C.c_double, C.c_float
+        P = C.POINTER
+        L.or_env_new.restype = vp
+        L.or_env_new.argtypes = [vp, i32, i32, i32, i32, i32, f64, f64, f64, u32]
+        L.or_env_free.argtypes = [vp]
+        L.or_env_reset.argtypes = [vp]
+        L.or_env_step.restype = i32
+        L.or_env_step.argtypes = [vp, vp, vp, P(f64), P(i32)]
+        L.or_env_get.argtypes = [vp, P(i32), P(f64), vp, vp]
+        L.or_trk_new.restype = vp
+        L.or_trk_new.argtypes = [i32]
+        L.or_trk_free.argtypes = [vp]
+        L.or_trk_clear.argtypes = [vp]
+        L.or_trk_get.restype = i32
+        L.or_trk_get.argtypes = [vp, vp]
+        L.or_trk_set.argtypes = [vp, vp, i32]
+        L.or_trk_update_from_env.argtypes = [vp, vp]
+        L.or_convert_observation.argtypes = [vp, i32, i32, i32, i32, vp, vp, i32, i32, vp]
+        L.or_generate_vector_features.argtypes = [i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp]
+        L.or_convert_global_state.argtypes = [vp, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, vp, vp]
+        L.or_compute_shaped_rewards.restype = f32
+        L.or_compute_shaped_rewards.argtypes = [f64, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp]
+        L.or_np_sum_f32.restype = f32
+        L.or_np_sum_f32.argtypes = [vp, i32]
+        L.or_batch_new.restype = vp
+        L.or_batch_new.argtypes = [i32, vp, i32, i32, i32, i32, i32, f64, f64, f64, u32, i32]
+        L.or_batch_free.argtypes = [vp]
+        L.or_batch_env.restype = vp
+        L.or_batch_env.argtypes = [vp, i32]
+        L.or_batch_trk.restype = vp
+        L.or_batch_trk.argtypes = [vp, i32]
+        L.or_batch_step.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class OracleEnv:
+    """``Environment`` restated in C (env.py:18-316)."""
+
+    def __init__(self, grid, n_robots, n_packages, max_time_steps, move_cost=-0.01, delivery_reward=10.0,
+                 delay_reward=1.0, seed=2025, _handle=None):
+        self.grid = _c(grid, np.uint8)
+        self.H, self.W = self.grid.shape
+        self.A, self.P, self.T = n_robots, n_packages, max_time_steps
+        self._owned = _handle is None
+        if _handle is None:
+            self.h = lib().or_env_new(_p(self.grid), self.H, self.W, n_robots, n_packages, max_time_steps,
+                                      move_cost, delivery_reward, delay_reward, seed & 0xFFFFFFFF)
+        else:
+            self.h = _handle
+
+    def __del__(self):
+        if getattr(self, "_owned", False) and getattr(self, "h", None):
+            lib().or_env_free(self.h)
+            self.h = None
+
+    def reset(self):
+        lib().or_env_reset(self.h)
+
+    def step(self, move_codes, op_codes):
+        mv = _c(move_codes, np.uint8)
+        op = _c(op_codes, np.uint8)
+        r = C.c_double()
+        ri = C.c_int()
+        d = lib().or_env_step(self.h, _p(mv), _p(op), C.byref(r), C.byref(ri))
+        return r.value, bool(ri.value), bool(d)
+
+    def state(self):
+        t = C.c_int()
+        tot = C.c_double()
+        rob = np.zeros((self.A, 3), np.int32)
+        pk = np.zeros((self.P, 8), np.int32)
+        lib().or_env_get(self.h, C.byref(t), C.byref(tot), _p(rob), _p(pk))
+        return dict(t=t.value, total_reward=tot.value, robots=rob, pkgs=pk)
+
+    def robots1(self):
+        s = self.state()
+        r = s["robots"].copy()
+        r[:, :2] += 1
+        return r
+
+
+class OracleTracker:
+    """Insertion-ordered persistent-package tracker (MAPPO/trainer.py:95-130)."""
+
+    def __init__(self, cap=64, _handle=None):
+        self._owned = _handle is None
+        self.h = lib().or_trk_new(cap) if _handle is None else _handle
+
+    def __del__(self):
+        if getattr(self, "_owned", False) and getattr(self, "h", None):
+            lib().or_trk_free(self.h)
+            self.h = None
+
+    def update_from_env(self, env: OracleEnv):
+        lib().or_trk_update_from_env(self.h, env.h)
+
+    def clear(self):
+        lib().or_trk_clear(self.h)
+
+    def rows(self, cap=4096):
+        out = np.zeros((cap, 8), np.int32)
+        n = lib().or_trk_get(self.h, _p(out))
+        return out[:n].copy()
+
+    def set(self, rows):
+        rows = _c(np.asarray(rows).reshape(-1, 8), np.int32)
+        lib().or_trk_set(self.h, _p(rows), rows.shape[0])
+
+
+def _trk(rows):
+    rows = _c(np.asarray(rows, dtype=np.int32).reshape(-1, 8), np.int32)
+    return rows, rows.shape[0]
+
+
+def convert_observation(grid, t, robots1, trk_rows, idx):
+    g = _c(grid, np.uint8)
+    H, W = g.shape
+    rb = _c(np.asarray(robots1).reshape(-1, 3), np.int32)
+    tr, n = _trk(trk_rows)
+    out = np.zeros((6, H, W), np.float32)
+    lib().or_convert_observation(_p(g), H, W, int(t), rb.shape[0], _p(rb), _p(tr), n, int(idx), _p(out))
+    return out
+
+
+def generate_vector_features(H, W, t, robots1, trk_rows, idx, T, MO, MP):
+    rb = _c(np.asarray(robots1).reshape(-1, 3), np.int32)
+    tr, n = _trk(trk_rows)
+    out = np.zeros(6 + 5 * MO + 5 * MP + 1, np.float32)
+    lib().or_generate_vector_features(H, W, int(t), rb.shape[0], _p(rb), _p(tr), n, int(idx), int(T), MO, MP, _p(out))
+    return out
+
+
+def convert_global_state(grid, t, robots1, trk_rows, T, MR, MPs):
+    g = _c(grid, np.uint8)
+    H, W = g.shape
+    rb = _c(np.asarray(robots1).reshape(-1, 3), np.int32)
+    tr, n = _trk(trk_rows)
+    gm = np.zeros((4, H, W), np.float32)
+    gv = np.zeros(6 * MR + 7 * MPs + 1, np.float32)
+    lib().or_convert_global_state(_p(g), H, W, int(t), rb.shape[0], _p(rb), _p(tr), n, int(T), MR, MPs, _p(gm), _p(gv))
+    return gm, gv
+
+
+def compute_shaped_rewards(g, prev_t, prev_robots1, cur_t, cur_robots1, move_codes, op_codes, trk_rows, A,
+                           consts=MAPPO_CONSTS):
+    pr = _c(np.asarray(prev_robots1).reshape(-1, 3), np.int32)
+    cr = _c(np.asarray(cur_robots1).reshape(-1, 3), np.int32)
+    mv = _c(move_codes, np.uint8)
+    op = _c(op_codes, np.uint8)
+    tr, n = _trk(trk_rows)
+    cs = _c(consts, np.float64)
+    return np.float32(lib().or_compute_shaped_rewards(float(g), int(prev_t), _p(pr), int(cur_t), _p(cr), _p(mv),
+                                                      _p(op), _p(tr), n, int(A), _p(cs)))
+
+
+def np_sum_f32(a):
+    a = _c(a, np.float32)
+    return np.float32(lib().or_np_sum_f32(_p(a), a.shape[0]))
+
+
+class OracleBatch:
+    """E envs run as the MAPPO rollout loop does (MAPPO/trainer.py:194-286, learner excluded)."""
+
+    def __init__(self, E, grid, A, P, T, move_cost=-0.01, delivery_reward=10.0, delay_reward=1.0, seed_base=42,
+                 clear_on_reset=False):
+        self.grid = _c(grid, np.uint8)
+        H, W = self.grid.shape
+        self.E, self.A, self.P, self.T = E, A, P, T
+        self.h = lib().or_batch_new(E, _p(self.grid), H, W, A, P, T, move_cost, delivery_reward, delay_reward,
+                                    seed_base & 0xFFFFFFFF, int(clear_on_reset))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_batch_free(self.h)
+            self.h = None
+
+    def env(self, e) -> OracleEnv:
+        o = OracleEnv.__new__(OracleEnv)
+        o.grid = self.grid
+        o.H, o.W = self.grid.shape
+        o.A, o.P, o.T = self.A, self.P, self.T
+        o._owned = False
+        o.h = lib().or_batch_env(self.h, e)
+        o._batch = self
+        return o
+
+    def tracker(self, e) -> OracleTracker:
+        t = OracleTracker(_handle=lib().or_batch_trk(self.h, e))
+        t._batch = self
+        return t
+
+    def step(self, actions_int, auto_reset=True, consts=MAPPO_CONSTS, n_threads=1):
+        a = _c(np.asarray(actions_int).reshape(self.E, self.A), np.uint8)
+        cs = _c(consts, np.float64)
+        r = np.zeros(self.E, np.float64)
+        sh = np.zeros(self.E, np.float32)
+        d = np.zeros(self.E, np.uint8)
+        lib().or_batch_step(self.h, _p(a), int(auto_reset), _p(cs), _p(r), _p(sh), _p(d), int(n_threads))
+        return r, sh, d.astype(bool)

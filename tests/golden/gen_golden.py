@@ -1,0 +1,556 @@
+"""Generate the golden fixtures under tests/golden/ by RUNNING the reference.
+
+Test infrastructure only.  This script runs in the build container, where the
+reference is mounted read-only at /root/reference; it never runs on the GPU box
+and nothing it imports is copied into the repository: only the data it writes
+(inputs and the reference's outputs) is committed.
+
+The reference is imported with a stub ``pygame`` module (env.py:2 imports it at
+module top; rendering is never called) and with bytecode writing disabled so
+the read-only tree stays untouched.
+
+Fixtures written (all small, compressed):
+  reset.npz         Environment.__init__ / reset() layouts       env.py:20-43, 81-125
+  steps.npz         Environment.step traces (incl. past done)    env.py:173-316
+  rollout_mappo.npz MAPPO rollout glue: decode, step, shaped reward,
+                    never-cleared tracker, auto-reset, obs/vec/global
+                    MAPPO/trainer.py:95-130,194-286, MAPPO/helper.py
+  rollout_qmix.npz  QMIX collection: subset stepping (indices=), fresh
+                    (cleared) tracker, QMIX dims/constants
+                    QMIX/trainer.py:333-526, QMIX/env_vectorized.py, QMIX/helper.py
+  helpers.npz       helper functions on hand-made/random dict inputs
+                    (odd trackers: stale entries, ids > P, start_time > t)
+  kat.json          notebook known-answer test (MAPPO/marl-delivery-mappo.ipynb cell 11)
+  eval_anchor.json  evaluation.run_eval('random'/'greedy') per-episode results
+                    for the README results table (README.md:117-121)
+
+Usage:  python tests/golden/gen_golden.py [--quick]
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+MAPS = os.path.join(REPO, "marl-delivery_amd", "marl_gpu", "maps")
+
+MOVE_CODES = {"S": 0, "L": 1, "R": 2, "U": 3, "D": 4}      # 5 = unknown string
+OP_CODES = {"0": 0, "1": 1, "2": 2}                       # 3 = '3' (numeric, no env effect)
+TRAINER_MOVES = None                                      # filled from sklearn LabelEncoder
+STATUS = {"None": 0, "waiting": 1, "in_transit": 2, "delivered": 3}
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_reference():
+    sys.modules.setdefault("pygame", types.ModuleType("pygame"))
+    ref = types.SimpleNamespace()
+    ref.env = _load("ref_env", os.path.join(REF, "env.py"))
+    ref.mappo_helper = _load("ref_mappo_helper", os.path.join(REF, "MAPPO", "helper.py"))
+    ref.qmix_helper = _load("ref_qmix_helper", os.path.join(REF, "QMIX", "helper.py"))
+    ref.vec = _load("ref_vec", os.path.join(REF, "MAPPO", "env_vectorized.py"))
+    ref.qvec = _load("ref_qvec", os.path.join(REF, "QMIX", "env_vectorized.py"))
+    # MAPPO trainer for its tracker update (module top-level only seeds RNGs)
+    sys.path.insert(0, os.path.join(REF, "MAPPO"))
+    sys.path.insert(1, REF)
+    ref.mappo_trainer = _load("ref_mappo_trainer", os.path.join(REF, "MAPPO", "trainer.py"))
+    ref.random_agent = _load("ref_randomagent", os.path.join(REF, "randomagent.py"))
+    ref.greedy_agent = _load("ref_greedyagent", os.path.join(REF, "greedyagent.py"))
+    from sklearn.preprocessing import LabelEncoder
+    le = LabelEncoder()
+    le.fit(["S", "L", "R", "U", "D"])
+    global TRAINER_MOVES
+    TRAINER_MOVES = [str(x) for x in le.classes_]
+    assert TRAINER_MOVES == ["D", "L", "R", "S", "U"], TRAINER_MOVES
+    return ref
+
+
+def map_file(name):
+    return os.path.join(MAPS, name)
+
+
+def decode_int(a):
+    """MAPPO/trainer.py:198-205 (LabelEncoder order D,L,R,S,U; op clamp)."""
+    a = int(a)
+    move = TRAINER_MOVES[a % 5]
+    op = a // 5
+    if op >= 3:
+        op = 0
+    return move, str(op)
+
+
+def enc_action(move, op):
+    return MOVE_CODES.get(move, 5), OP_CODES.get(op, 3)
+
+
+def env_arrays(env):
+    pos = np.array([r.position for r in env.robots], dtype=np.int16).reshape(-1, 2)
+    carry = np.array([r.carrying for r in env.robots], dtype=np.int16)
+    pk = np.array([(p.start[0], p.start[1], p.target[0], p.target[1], p.start_time, p.deadline)
+                   for p in env.packages], dtype=np.int32).reshape(-1, 6)
+    st = np.array([STATUS[p.status] for p in env.packages], dtype=np.uint8)
+    return pos, carry, pk, st
+
+
+# ----------------------------------------------------------------------------
+def gen_reset(ref, quick):
+    cases = []
+    arrays = {}
+    maps = ["map.txt", "map1.txt", "map2.txt", "map3.txt", "map4.txt", "map5.txt", "synthetic64.txt"]
+    combos = []
+    for m in maps:
+        for A, P, T in [(1, 1, 100), (2, 5, 100), (5, 20, 100), (5, 50, 500), (5, 100, 1000),
+                        (16, 100, 500), (3, 7, 2), (8, 30, 40)]:
+            combos.append((m, A, P, T))
+    combos.append(("map1.txt", 40, 60, 300))
+    combos.append(("map3.txt", 64, 200, 1000))
+    combos.append(("synthetic64.txt", 64, 1000, 2000))
+    seeds = [0, 7, 42, 2025, 4294967295]
+    i = 0
+    for (m, A, P, T) in combos:
+        for s in (seeds[:2] if quick else seeds):
+            env = ref.env.Environment(map_file(m), T, A, P, seed=s)
+            rob, pk = [], []
+            for d in range(3):
+                if d > 0:
+                    env.reset()
+                pos, _, pkt, _ = env_arrays(env)
+                rob.append(pos)
+                pk.append(pkt)
+            arrays[f"robots_{i}"] = np.stack(rob).astype(np.uint8)
+            arrays[f"pkgs_{i}"] = np.stack(pk).astype(np.int32)
+            cases.append(dict(map=m, A=A, P=P, T=T, seed=s))
+            i += 1
+    arrays["meta"] = np.frombuffer(json.dumps(cases).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "reset.npz"), **arrays)
+    print("reset cases", len(cases))
+
+
+def gen_steps(ref, quick):
+    cases = [
+        # map, A, P, T, seed, act_seed, nsteps, auto_reset, odd_strings
+        ("map1.txt", 5, 50, 500, 42, 1, 700, False, False),
+        ("map1.txt", 5, 20, 60, 2025, 2, 200, True, False),
+        ("map.txt", 2, 5, 30, 3, 3, 120, True, True),
+        ("map1.txt", 30, 20, 200, 11, 4, 250, False, False),
+        ("map1.txt", 40, 10, 100, 12, 5, 150, False, False),
+        ("map3.txt", 40, 60, 150, 13, 6, 200, False, True),
+        ("map2.txt", 16, 100, 120, 14, 7, 260, True, False),
+        ("map4.txt", 5, 50, 80, 15, 8, 200, True, False),
+        ("map5.txt", 8, 30, 60, 16, 9, 150, True, False),
+        ("synthetic64.txt", 16, 100, 100, 17, 10, 120, True, False),
+        ("map1.txt", 64, 3, 50, 18, 11, 60, False, False),
+        ("map1.txt", 3, 4, 5, 19, 12, 40, False, False),   # all-delivered unlikely; t past T
+    ]
+    if quick:
+        cases = cases[:3]
+    arrays = {}
+    meta = []
+    for ci, (m, A, P, T, seed, aseed, n, auto, odd) in enumerate(cases):
+        env = ref.env.Environment(map_file(m), T, A, P, seed=seed)
+        env.reset()
+        rs = np.random.RandomState(aseed)
+        acts = np.zeros((n, A, 2), np.uint8)
+        pos_l, car_l, st_l, pk_l = [], [], [], []
+        r_l, rint_l, done_l, t_l, tot_l = [], [], [], [], []
+        pos0, car0, pk0, st0 = env_arrays(env)
+        for k in range(n):
+            ints = rs.randint(0, 15, size=A)
+            actions = [decode_int(a) for a in ints]
+            if odd:
+                for a in range(A):
+                    u = rs.random_sample()
+                    if u < 0.05:
+                        actions[a] = ("X", actions[a][1])
+                    elif u < 0.10:
+                        actions[a] = (actions[a][0], "3")
+            for a in range(A):
+                acts[k, a] = enc_action(*actions[a])
+            _, r, done, infos = env.step(actions)
+            if done:
+                assert infos["total_reward"] == env.total_reward and infos["total_time_steps"] == env.t
+            r_l.append(float(r))
+            rint_l.append(isinstance(r, int))
+            done_l.append(bool(done))
+            tot_l.append(float(env.total_reward))
+            t_l.append(env.t)
+            if done and auto:
+                env.reset()
+            pos, car, pk, st = env_arrays(env)
+            pos_l.append(pos); car_l.append(car); st_l.append(st); pk_l.append(pk)
+        arrays[f"acts_{ci}"] = acts
+        arrays[f"pos0_{ci}"] = pos0.astype(np.uint8)
+        arrays[f"carry0_{ci}"] = car0
+        arrays[f"pkgs0_{ci}"] = pk0
+        arrays[f"status0_{ci}"] = st0
+        arrays[f"pos_{ci}"] = np.stack(pos_l).astype(np.uint8)
+        arrays[f"carry_{ci}"] = np.stack(car_l).astype(np.uint16)
+        arrays[f"status_{ci}"] = np.stack(st_l)
+        arrays[f"pkgs_{ci}"] = np.stack(pk_l)
+        arrays[f"r_{ci}"] = np.array(r_l, np.float64)
+        arrays[f"rint_{ci}"] = np.array(rint_l, np.bool_)
+        arrays[f"done_{ci}"] = np.array(done_l, np.bool_)
+        arrays[f"t_{ci}"] = np.array(t_l, np.int32)
+        arrays[f"total_{ci}"] = np.array(tot_l, np.float64)
+        meta.append(dict(map=m, A=A, P=P, T=T, seed=seed, act_seed=aseed, n=n, auto_reset=auto, odd=odd))
+    arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "steps.npz"), **arrays)
+    print("step cases", len(meta))
+
+
+# ----------------------------------------------------------------------------
+class _Trk:
+    """Holder for the reference tracker-update method (needs ``self.persistent_packages_list``)."""
+
+    def __init__(self, n):
+        self.persistent_packages_list = [{} for _ in range(n)]
+
+
+def tracker_update(ref, holder, e, state):
+    ref.mappo_trainer.MAPPOTrainer._update_persistent_packages_for_env(holder, e, state)
+
+
+def gen_rollout_mappo(ref, quick, tag, mapname, E, A, P, T, seed, K, MO, MP, MR, MPs, big_every, map_every):
+    H = ref.mappo_helper
+    Q = ref.qmix_helper
+    vec = ref.vec.VectorizedEnv(ref.env.Environment, num_envs=E, map_file=map_file(mapname), n_robots=A,
+                                n_packages=P, move_cost=-0.01, delivery_reward=10, delay_reward=1,
+                                seed=seed, max_time_steps=T)
+    trk = _Trk(E)
+    states = vec.reset()
+    for e in range(E):
+        tracker_update(ref, trk, e, states[e])
+    rs = np.random.RandomState(seed + 1000)
+    nr, nc = vec.envs[0].n_rows, vec.envs[0].n_cols
+    Dv = 6 + 5 * MO + 5 * MP + 1
+    Dg = 6 * MR + 7 * MPs + 1
+    n_obs = K + 1
+    map_steps = [k for k in range(n_obs) if k % map_every == 0]
+    big_steps = [k for k in range(n_obs) if k % big_every == 0]
+    amap = np.zeros((len(map_steps), E, A, 6, nr, nc), np.uint8)
+    cmap = np.zeros((len(map_steps), E, 4, nr, nc), np.uint8)
+    avec = np.zeros((n_obs, E, A, Dv), np.float32)
+    avec_big = np.zeros((len(big_steps), E, A, 6 + 5 * 100 + 5 * 100 + 1), np.float32)
+    cvec = np.zeros((n_obs, E, Dg), np.float32)
+    cvec_q = np.zeros((n_obs, E, 6 * 10 + 7 * 20 + 1), np.float32)
+    acts = np.zeros((K, E, A), np.uint8)
+    r_env = np.zeros((K, E), np.float64)
+    r_sh = np.zeros((K, E), np.float32)
+    r_shq = np.zeros((K, E), np.float32)
+    dones = np.zeros((K, E), np.bool_)
+
+    def record(k, sts):
+        for e in range(E):
+            tr = trk.persistent_packages_list[e]
+            for a in range(A):
+                avec[k, e, a] = H.generate_vector_features(sts[e], tr, a, T, MO, MP)
+                if k in map_steps:
+                    amap[map_steps.index(k), e, a] = H.convert_observation(sts[e], tr, a).astype(np.uint8)
+                if k in big_steps:
+                    avec_big[big_steps.index(k), e, a] = H.generate_vector_features(sts[e], tr, a, T)
+            gm, gv = H.convert_global_state(sts[e], tr, T, MR, MPs)
+            cvec[k, e] = gv
+            _, gq = Q.convert_global_state(sts[e], tr, T, 10, 20)
+            cvec_q[k, e] = gq
+            if k in map_steps:
+                cmap[map_steps.index(k), e] = gm.astype(np.uint8)
+
+    record(0, states)
+    for k in range(K):
+        ints = rs.randint(0, 15, size=(E, A))
+        acts[k] = ints
+        env_actions = [[decode_int(a) for a in ints[e]] for e in range(E)]
+        nxt, rews, dns, _ = vec.step(env_actions)
+        for e in range(E):
+            tr_prev = trk.persistent_packages_list[e]
+            r_sh[k, e] = H.compute_shaped_rewards(rews[e], states[e], nxt[e], env_actions[e], tr_prev, A)
+            r_shq[k, e] = Q.compute_shaped_rewards(rews[e], states[e], nxt[e], env_actions[e], tr_prev, A)
+            r_env[k, e] = float(rews[e])
+            dones[k, e] = bool(dns[e])
+        for e in range(E):
+            if dns[e]:
+                rst = vec.envs[e].reset()
+                tracker_update(ref, trk, e, rst)           # never cleared (trainer.py:232-233)
+                nxt[e] = rst
+            else:
+                tracker_update(ref, trk, e, nxt[e])
+        states = list(nxt)
+        record(k + 1, states)
+    np.savez_compressed(
+        os.path.join(HERE, f"rollout_{tag}.npz"),
+        acts=acts, r_env=r_env, r_shaped=r_sh, r_shaped_qmix=r_shq, done=dones,
+        amap=amap, cmap=cmap, avec=avec, avec_big=avec_big, cvec=cvec, cvec_qmix=cvec_q,
+        map_steps=np.array(map_steps, np.int32), big_steps=np.array(big_steps, np.int32),
+        meta=np.frombuffer(json.dumps(dict(map=mapname, E=E, A=A, P=P, T=T, seed=seed, K=K, MO=MO, MP=MP,
+                                           MR=MR, MPs=MPs, act_seed=seed + 1000)).encode(), dtype=np.uint8))
+    print("rollout", tag, "dones", int(dones.sum()))
+
+
+def gen_rollout_qmix(ref, quick):
+    """QMIX/trainer.py:333-526 collection semantics with random actions (no learner)."""
+    Q = ref.qmix_helper
+    E, A, P, T, seed = 4, 5, 20, 50, 42
+    MO, MP, MR, MPs = 4, 5, 10, 20
+    iters = 2
+    vec = ref.qvec.VectorizedEnv(ref.env.Environment, num_envs=E, map_file=map_file("map1.txt"), n_robots=A,
+                                 n_packages=P, move_cost=-0.01, delivery_reward=10, delay_reward=1,
+                                 seed=seed, max_time_steps=T)
+    trk = _Trk(E)
+    states = vec.reset()
+    for e in range(E):
+        tracker_update(ref, trk, e, states[e])
+    rs = np.random.RandomState(7)
+    rec = dict(active=[], acts=[], r=[], sh=[], done=[], avec=[], cvec=[], amap=[])
+    for it in range(iters):
+        active = [True] * E
+        prev = [s.copy() for s in states]
+        for tstep in range(T + 5):
+            idx = [e for e in range(E) if active[e]]
+            if not idx:
+                break
+            ints = rs.randint(0, 15, size=(E, A))
+            env_actions = [[decode_int(a) for a in ints[e]] for e in idx]
+            nxt, rews, terms, _ = vec.step(env_actions, idx)
+            act_mask = np.zeros(E, np.bool_)
+            act_mask[idx] = True
+            r_row = np.zeros(E, np.float64)
+            sh_row = np.zeros(E, np.float32)
+            d_row = np.zeros(E, np.bool_)
+            for j, e in enumerate(idx):
+                sh_row[e] = Q.compute_shaped_rewards(rews[j], states[e], nxt[j], env_actions[j],
+                                                     trk.persistent_packages_list[e], A)
+                tracker_update(ref, trk, e, nxt[j])
+                r_row[e] = float(rews[j])
+                d_row[e] = bool(terms[j])
+                states[e] = nxt[j]
+                if terms[j]:
+                    active[e] = False
+            av = np.zeros((E, A, 6 + 5 * MO + 5 * MP + 1), np.float32)
+            cv = np.zeros((E, 6 * MR + 7 * MPs + 1), np.float32)
+            am = np.zeros((E, A, 6, 10, 10), np.uint8)
+            for e in range(E):
+                tr = trk.persistent_packages_list[e]
+                for a in range(A):
+                    av[e, a] = Q.generate_vector_features(states[e], tr, a, T, MO, MP)
+                    am[e, a] = Q.convert_observation(states[e], tr, a).astype(np.uint8)
+                cv[e] = Q.convert_global_state(states[e], tr, T, MR, MPs)[1]
+            rec["active"].append(act_mask); rec["acts"].append(ints.astype(np.uint8)); rec["r"].append(r_row)
+            rec["sh"].append(sh_row); rec["done"].append(d_row); rec["avec"].append(av); rec["cvec"].append(cv)
+            rec["amap"].append(am)
+        # end of iteration: reset all + clear trackers (QMIX/trainer.py:523-526)
+        states = vec.reset()
+        trk.persistent_packages_list = [{} for _ in range(E)]
+        for e in range(E):
+            tracker_update(ref, trk, e, states[e])
+        rec["active"].append(np.zeros(E, np.bool_)); rec["acts"].append(np.zeros((E, A), np.uint8))
+        rec["r"].append(np.zeros(E)); rec["sh"].append(np.zeros(E, np.float32)); rec["done"].append(np.zeros(E, np.bool_))
+        av = np.zeros((E, A, 6 + 5 * MO + 5 * MP + 1), np.float32)
+        cv = np.zeros((E, 6 * MR + 7 * MPs + 1), np.float32)
+        am = np.zeros((E, A, 6, 10, 10), np.uint8)
+        for e in range(E):
+            tr = trk.persistent_packages_list[e]
+            for a in range(A):
+                av[e, a] = Q.generate_vector_features(states[e], tr, a, T, MO, MP)
+                am[e, a] = Q.convert_observation(states[e], tr, a).astype(np.uint8)
+            cv[e] = Q.convert_global_state(states[e], tr, T, MR, MPs)[1]
+        rec["avec"].append(av); rec["cvec"].append(cv); rec["amap"].append(am)
+    out = {k: np.stack(v) for k, v in rec.items()}
+    out["meta"] = np.frombuffer(json.dumps(dict(map="map1.txt", E=E, A=A, P=P, T=T, seed=seed, MO=MO, MP=MP,
+                                                 MR=MR, MPs=MPs, iters=iters, act_seed=7)).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "rollout_qmix.npz"), **out)
+    print("qmix rows", len(rec["active"]))
+
+
+# ----------------------------------------------------------------------------
+def random_dict_case(rs, grid, A, n_trk, t, id_max):
+    """A random state dict + tracker with deliberately odd entries."""
+    H, W = len(grid), len(grid[0])
+    free = [(i, j) for i in range(H) for j in range(W) if grid[i][j] == 0]
+    cells = rs.permutation(len(free))
+    robots = []
+    ids = list(rs.permutation(np.arange(1, id_max + 1))[:n_trk])
+    trk = {}
+    for k, pid in enumerate(ids):
+        s = free[rs.randint(len(free))]
+        tg = free[rs.randint(len(free))]
+        st = int(rs.randint(0, t + 20))
+        dl = int(st + rs.randint(0, 40))
+        status = "in_transit" if rs.random_sample() < 0.3 else "waiting"
+        trk[int(pid)] = {"id": int(pid), "start_pos": (s[0], s[1]), "target_pos": (tg[0], tg[1]),
+                         "start_time": st, "deadline": dl, "status": status}
+    carried = [k for k, v in trk.items() if v["status"] == "in_transit"]
+    for a in range(A):
+        r, c = free[cells[a]]
+        u = rs.random_sample()
+        if carried and u < 0.5:
+            cy = carried.pop()
+        elif u < 0.6:
+            cy = int(rs.randint(1, id_max + 5))       # carried id possibly not in tracker
+        else:
+            cy = 0
+        robots.append((r + 1, c + 1, cy))
+    return {"time_step": int(t), "map": grid, "robots": robots, "packages": []}, trk
+
+
+def gen_helpers(ref, quick):
+    H = ref.mappo_helper
+    Q = ref.qmix_helper
+    rs = np.random.RandomState(99)
+    cases = []
+    arrays = {}
+    grids = {m: ref.env.Environment(map_file(m), 10, 1, 1, seed=0).grid for m in ["map1.txt", "map2.txt", "map.txt"]}
+    n = 40 if quick else 160
+    for i in range(n):
+        m = ["map1.txt", "map2.txt", "map.txt"][i % 3]
+        grid = grids[m]
+        A = int(rs.choice([1, 2, 5, 8]))
+        n_trk = int(rs.randint(0, 25))
+        t = int(rs.randint(0, 120))
+        state, trk = random_dict_case(rs, grid, A, n_trk, t, id_max=30)
+        Tn = int(rs.choice([0, 50, 100, 500]))
+        MO, MP, MR, MPs = [int(x) for x in rs.choice([1, 3, 4, 100], 4)]
+        MR = max(MR, 1)
+        idx = int(rs.randint(-1, A + 1))
+        obs = H.convert_observation(state, trk, idx)
+        vec = H.generate_vector_features(state, trk, idx, Tn, MO, MP)
+        gm, gv = H.convert_global_state(state, trk, Tn, MR, MPs)
+        # shaped reward: current = prev with robots moved/carry changed at random
+        cur = dict(state)
+        cur_robots = []
+        free = [(a, b) for a in range(len(grid)) for b in range(len(grid[0])) if grid[a][b] == 0]
+        for (r, c, cy) in state["robots"]:
+            u = rs.random_sample()
+            if u < 0.4:
+                fr = free[rs.randint(len(free))]
+                r, c = fr[0] + 1, fr[1] + 1
+            if rs.random_sample() < 0.3:
+                cy = 0 if cy else int(rs.randint(1, 31))
+            cur_robots.append((r, c, cy))
+        cur["robots"] = cur_robots
+        cur["time_step"] = t + 1
+        acts = [("SLRUDX"[rs.randint(6)], "0123"[rs.randint(4)]) for _ in range(A)]
+        g = float(rs.choice([0.0, -0.05, 9.97, 1.0, -0.01]))
+        g_int = bool(rs.random_sample() < 0.2)
+        gval = 0 if g_int else g
+        sh_m = H.compute_shaped_rewards(gval, state, cur, acts, trk, A)
+        sh_q = Q.compute_shaped_rewards(gval, state, cur, acts, trk, A)
+        trk_rows = np.array([[v["id"], 1 if v["status"] == "waiting" else 2, v["start_pos"][0], v["start_pos"][1],
+                              v["target_pos"][0], v["target_pos"][1], v["start_time"], v["deadline"]]
+                             for v in trk.values()], np.int32).reshape(-1, 8)
+        arrays[f"robots_{i}"] = np.array(state["robots"], np.int32).reshape(-1, 3)
+        arrays[f"cur_robots_{i}"] = np.array(cur_robots, np.int32).reshape(-1, 3)
+        arrays[f"trk_{i}"] = trk_rows
+        arrays[f"acts_{i}"] = np.array([enc_action(*a) for a in acts], np.uint8).reshape(-1, 2)
+        arrays[f"obs_{i}"] = obs.astype(np.uint8)
+        arrays[f"vec_{i}"] = vec
+        arrays[f"gmap_{i}"] = gm.astype(np.uint8)
+        arrays[f"gvec_{i}"] = gv
+        arrays[f"sh_{i}"] = np.array([sh_m, sh_q], np.float32)
+        cases.append(dict(map=m, A=A, t=t, T=Tn, idx=idx, MO=MO, MP=MP, MR=MR, MPs=MPs, g=g, g_int=g_int))
+    arrays["meta"] = np.frombuffer(json.dumps(cases).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "helpers.npz"), **arrays)
+    print("helper cases", len(cases))
+
+
+def gen_kat(ref):
+    prev = {"robots": [(2, 2, 0), (5, 5, 1)], "time_step": 4}
+    cur = {"robots": [(3, 2, 2), (5, 4, 0)], "time_step": 5}
+    acts = [("D", "1"), ("L", "2")]
+    trk = {1: {"id": 1, "start_pos": (0, 0), "target_pos": (4, 3), "start_time": 0, "deadline": 10, "status": "in_transit"},
+           2: {"id": 2, "start_pos": (2, 1), "target_pos": (0, 4), "start_time": 3, "deadline": 15, "status": "waiting"}}
+    m = ref.mappo_helper.compute_shaped_rewards(10, prev, cur, acts, trk, 2)
+    q = ref.qmix_helper.compute_shaped_rewards(10, prev, cur, acts, trk, 2)
+    out = dict(source="MAPPO/marl-delivery-mappo.ipynb code cell 11 (recorded output 215.04000854492188)",
+               prev_robots=prev["robots"], prev_t=4, cur_robots=cur["robots"], cur_t=5,
+               actions=acts, global_reward=10,
+               tracker=[[v["id"], 2 if v["status"] == "in_transit" else 1, *v["start_pos"], *v["target_pos"],
+                         v["start_time"], v["deadline"]] for v in trk.values()],
+               mappo=float(m), mappo_f32_hex=np.float32(m).tobytes().hex(),
+               qmix=float(q), qmix_f32_hex=np.float32(q).tobytes().hex(), notebook_recorded=215.04000854492188)
+    assert float(m) == 215.04000854492188
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("kat", m, q)
+
+
+def gen_eval_anchor(ref, quick):
+    """evaluation.py:9-66 for the README table settings (README.md:110,117-121,176)."""
+    import contextlib
+    import io
+    cfg = dict(map=map_file("map1.txt"), max_time_steps=1000, n_agents=5, n_packages=100, seed=10)
+    eps = 10 if quick else 100
+    res = {}
+    for kind in ("random", "greedy"):
+        np.random.seed(10)
+        rewards, delivered = [], []
+        for ep in range(eps):
+            env = ref.env.Environment(map_file=cfg["map"], max_time_steps=cfg["max_time_steps"],
+                                      n_robots=cfg["n_agents"], n_packages=cfg["n_packages"], seed=cfg["seed"] + ep)
+            state = env.reset()
+            agent = ref.random_agent.RandomAgents() if kind == "random" else ref.greedy_agent.GreedyAgents()
+            agent.init_agents(state)
+            done = False
+            infos = {}
+            with contextlib.redirect_stdout(io.StringIO()):
+                while not done:
+                    actions = agent.get_actions(state, deterministic=True) if kind == "random" else agent.get_actions(state)
+                    state, reward, done, infos = env.step(actions)
+            rewards.append(float(infos.get("total_reward", env.total_reward)))
+            delivered.append(int(sum(1 for p in env.packages if p.status == "delivered")))
+        res[kind] = dict(rewards=rewards, delivered=delivered, mean_reward=float(np.mean(rewards)),
+                         std_reward=float(np.std(rewards)), mean_delivered=float(np.mean(delivered)),
+                         std_delivered=float(np.std(delivered)))
+        print(kind, res[kind]["mean_reward"], res[kind]["std_reward"], res[kind]["mean_delivered"])
+    res["config"] = dict(map="map1.txt", max_time_steps=1000, n_agents=5, n_packages=100, seed=10, episodes=eps,
+                         readme="README.md:117-121")
+    with open(os.path.join(HERE, "eval_anchor.json"), "w") as f:
+        json.dump(res, f)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    ref = load_reference()
+    todo = args.only.split(",") if args.only else ["reset", "steps", "mappo", "qmix", "helpers", "kat", "eval"]
+    if "reset" in todo:
+        gen_reset(ref, args.quick)
+    if "steps" in todo:
+        gen_steps(ref, args.quick)
+    if "mappo" in todo:
+        gen_rollout_mappo(ref, args.quick, "mappo", "map1.txt", E=3, A=5, P=50, T=60, seed=42, K=130,
+                          MO=4, MP=5, MR=100, MPs=100, big_every=10, map_every=1)
+        gen_rollout_mappo(ref, args.quick, "mappo_map2", "map2.txt", E=2, A=5, P=50, T=80, seed=7, K=100,
+                          MO=4, MP=5, MR=100, MPs=100, big_every=20, map_every=5)
+        gen_rollout_mappo(ref, args.quick, "mappo_syn64", "synthetic64.txt", E=2, A=16, P=100, T=60, seed=5, K=70,
+                          MO=15, MP=20, MR=16, MPs=100, big_every=35, map_every=35)
+    if "qmix" in todo:
+        gen_rollout_qmix(ref, args.quick)
+    if "helpers" in todo:
+        gen_helpers(ref, args.quick)
+    if "kat" in todo:
+        gen_kat(ref)
+    if "eval" in todo:
+        gen_eval_anchor(ref, args.quick)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,237 @@
+"""Benchmark of the marl-delivery hot path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): map1.txt, 5 agents, 4096 batched envs per
+GPU, step + reward kernel: one ``mdl_step`` per env-step = movement with
+shared-cell priority, package pickup/drop/spawn, fp64 env reward, float32
+MAPPO shaped reward with the never-cleared tracker, tracker update and
+reset-on-done.  P=50 packages, T=500 (MAPPO/trainer.py:41-47), env seeds
+42 + global env index, actions uint8 uniform in [0, 15) pre-generated on the
+device (Philox, seed 0) -- inputs resident in HBM before the timed region.
+
+A "step" = one ``mdl_step`` over all local envs.  The K timed steps are
+replayed from hipGraphs of G steps each (launch-bound loop; the same kernels
+as eager launches).  value = agent-steps/s over all ranks (weak scaling: 4096
+envs per GPU, no collective on the step path).
+
+Extra fields: eager (un-captured) throughput, the roofline record of the step
+kernel (HIP-event timed), and the CPU baseline (the oracle's C restatement,
+single thread, on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "marl-delivery_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+STEP_BYTES_PER_ENV = lambda A, P: 9 * A + 10 * P + 41  # SURVEY.md §8(d) / A.7  # noqa: E731
+HBM_PEAK_GBS = 8000.0                                     # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--map", default="map1.txt")
+    ap.add_argument("--agents", type=int, default=5)
+    ap.add_argument("--packages", type=int, default=50)
+    ap.add_argument("--T", type=int, default=500)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--graph-steps", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--no-graph", action="store_true", help="eager launches only (PMC profiling passes)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, grid, seeds0, budget_s):
+    """The oracle's C restatement (single thread) on the same workload: the first
+    rank's envs, same seeds and the same action stream, for as many steps as fit
+    in ~budget_s of CPU time."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    E, A = args.envs, args.agents
+    ob = O.OracleBatch(E, grid, A, args.packages, args.T, seed_base=int(seeds0), clear_on_reset=False)
+    gen = torch.Generator().manual_seed(0)
+    t_all = 0.0
+    steps = 0
+    while t_all < budget_s:
+        ints = torch.randint(0, 15, (E, A), generator=gen, dtype=torch.uint8).numpy()
+        t0 = time.perf_counter()
+        ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS, n_threads=1)
+        t_all += time.perf_counter() - t0
+        steps += 1
+    cpu_model = platform.processor()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": E * A * steps / t_all, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{E} envs x {steps} steps ({E * A * steps} agent-steps, {t_all:.1f} s) of the same workload, "
+                      f"oracle/mdl_oracle.c single thread, host {cpu_model}"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import marl_gpu
+    from marl_gpu.maps import grid_array, load_map, map_path
+    grid = grid_array(load_map(map_path(args.map)))
+    E, A, P = args.envs, args.agents, args.packages
+    seed0 = args.seed + rank * E                                  # global env index -> seed
+    env = marl_gpu.BatchedEnv(grid, E, A, P, args.T, seed=seed0, tracker="mappo", shaping="mappo",
+                              max_packages_obs=5, device=dev)
+    env.reset()
+
+    G = max(1, min(args.graph_steps, args.steps))
+    n_graph = (args.steps + G - 1) // G
+    K = n_graph * G
+    gen = torch.Generator(device=dev).manual_seed(0 + rank)
+    acts = torch.randint(0, 15, (G, E, A), generator=gen, device=dev, dtype=torch.int32).to(torch.uint8)
+    r = torch.zeros(E, dtype=torch.float64, device=dev)
+    sh = torch.zeros(E, dtype=torch.float32, device=dev)
+    dn = torch.zeros(E, dtype=torch.uint8, device=dev)
+
+    def one(k):
+        env.step(acts[k % G], auto_reset=True, out=(r, sh, dn))
+
+    # warmup (eager)
+    for k in range(args.warmup):
+        one(k)
+    torch.cuda.synchronize()
+
+    # capture G steps in a hipGraph (torch's stream capture covers the ctypes launches)
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream())
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            one(0)  # prime on the side stream
+            torch.cuda.synchronize()
+            with torch.cuda.graph(graph, stream=s):
+                for k in range(G):
+                    one(k)
+        torch.cuda.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---- timed region: K steps replayed from graphs ----
+    barrier()
+    t0 = time.perf_counter()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    if graph is not None:
+        for _ in range(n_graph):
+            graph.replay()
+    else:
+        for k in range(K):
+            one(k)
+    ev1.record()
+    barrier()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+
+    # ---- eager throughput (same kernels, one ctypes launch per step) ----
+    barrier()
+    t1 = time.perf_counter()
+    for k in range(K):
+        one(k)
+    barrier()
+    wall_eager = time.perf_counter() - t1
+
+    # ---- per-launch kernel duration with HIP events on the launch stream ----
+    nk = min(K, 500)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
+    for k in range(nk):
+        starts[k].record()
+        one(k)
+        ends[k].record()
+    torch.cuda.synchronize()
+    kdur_us = float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]) * 1e3)
+
+    if dist is not None:
+        t = torch.tensor([wall, wall_eager], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, wall_eager = float(t[0]), float(t[1])
+
+    total_agent_steps = E * A * K * world
+    value = total_agent_steps / wall
+    if rank == 0:
+        per_launch_bytes = STEP_BYTES_PER_ENV(A, P) * E
+        achieved = per_launch_bytes / (kdur_us * 1e-6) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("config") == {"envs": E, "agents": A, "packages": P, "map": args.map}:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(args, grid, seed0, args.cpu_seconds)
+        out = {
+            "metric": "agent-steps/sec (whole node), map1 5-agent 4096 envs, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": wall / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32+fp64",
+            "data": "synthetic: uniform random trainer-int actions (Philox, on device), env seeds 42+global index",
+            "config": {"workload": f"{args.map} A={A} P={P} T={args.T} {E} envs/GPU, mdl_step "
+                                   "(move+packages+env reward+MAPPO shaped reward+tracker+auto-reset), "
+                                   + ("eager launches" if graph is None else "hipGraph replay"),
+                       "envs_per_gpu": E, "agents": A, "packages": P, "max_time_steps": args.T,
+                       "parallelism": f"env-shard x{world}"},
+            "gpu_event_ms_per_step": gpu_ms / K,
+            "eager": {"value": total_agent_steps / wall_eager, "ms_per_step": wall_eager / K * 1e3},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "mdl::k_step<true>", "kernel_us": kdur_us,
+                         "algorithmic_bytes_per_launch": per_launch_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    env.close()
+
+
+if __name__ == "__main__":
+    main()

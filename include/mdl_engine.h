@@ -1,0 +1,157 @@
+/*
+ * mdl_engine.h -- C ABI of the MI355X-native marl-delivery batched step engine.
+ *
+ * One engine = E independent grid-world instances resident in HBM on one GPU.
+ * All compute runs as gfx950 HIP kernels, one wavefront per env instance.
+ * Entry points are extern "C", take plain pointers and sizes, and return an
+ * int status (0 = ok, <0 = error; mdl_last_error() gives a thread-local
+ * message).  No exception crosses the ABI.  Every call that takes a `stream`
+ * (a hipStream_t passed as void*, NULL = default stream) is asynchronous on
+ * that stream; device pointers are caller-owned unless documented otherwise.
+ * One engine per device; calls on one handle are not thread-safe.
+ *
+ * The reference has no FFI (it is pure Python); each entry point below names
+ * the Python interface it replaces (path:line under the reference tree).
+ * INTEGRATION.md shows the ctypes binding a maintainer of the reference
+ * would add.
+ */
+#ifndef MDL_ENGINE_H
+#define MDL_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDL_MAX_ROBOTS 64      /* one wavefront lane per robot */
+#define MDL_MAX_PACKAGES 1024  /* Group-Project.pdf p.3 bounds G <= 1000 */
+#define MDL_MAX_CELLS 16384    /* H*W <= 128*128; H, W <= 255 */
+
+/* tracker semantics of the persistent-package dict */
+#define MDL_TRACKER_FRESH 0        /* == env truth; QMIX/trainer.py:523-526 clears it on reset */
+#define MDL_TRACKER_MAPPO_STALE 1  /* MAPPO/trainer.py:232-233 never clears it on auto-reset */
+
+/* action byte formats for mdl_step */
+#define MDL_ACTION_TRAINER_INT 0   /* int a: move=['D','L','R','S','U'][a%5], op=a//5 (>=3 -> 0); MAPPO/trainer.py:198-205 */
+#define MDL_ACTION_CODES 1         /* move code | op code << 3; move 0..5 = S,L,R,U,D,<other string>; op 0..3 = '0','1','2',<other int> */
+
+typedef struct MdlEngine MdlEngine;
+
+/* Environment(...) constructor arguments (env.py:20-22) + the featurizer /
+ * shaping configuration of the trainers (MAPPO/trainer.py:39-64,
+ * MAPPO/helper.py:68-70,167-169,271-279, QMIX/config.yaml). */
+typedef struct {
+    int32_t n_envs;            /* E */
+    int32_t n_robots;          /* A, 1..64 */
+    int32_t n_packages;        /* P, 1..1024 */
+    int32_t max_time_steps;    /* T */
+    double move_cost;          /* env.py:21 defaults -0.01 */
+    double delivery_reward;    /* 10.0 */
+    double delay_reward;       /* 1.0 */
+    int32_t tracker_mode;      /* MDL_TRACKER_* */
+    double shaping[9];         /* pickup, on_time, late, closer, wasted_pick, wasted_drop, stuck, idle, away */
+    int32_t obs_max_time_steps;/* T passed to the feature builders */
+    int32_t max_other_robots;  /* MO  (generate_vector_features) */
+    int32_t max_packages_obs;  /* MP */
+    int32_t max_robots_state;  /* MR  (convert_global_state) */
+    int32_t max_packages_state;/* MPs */
+} MdlConfig;
+
+/* Create an engine on `device`.  grids: n_maps row-major 0/1 maps packed back
+ * to back; map_hw: 2*n_maps (H, W); env_map: E map indices (NULL = all map 0).
+ * Replaces Environment.__init__ / load_map (env.py:20-57) and
+ * VectorizedEnv.__init__ (MAPPO/env_vectorized.py:2-11) minus seeding. */
+int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw, int32_t n_maps,
+               const int32_t* env_map, int32_t device, MdlEngine** out);
+int mdl_destroy(MdlEngine* eng);
+
+/* RandomState(seed) (env.py:40) for every env -- seeds: E host uint32 -- then
+ * the constructor's layout draw (env.py:41).  VectorizedEnv passes seed+i
+ * (MAPPO/env_vectorized.py:8-9). */
+int mdl_seed(MdlEngine* eng, const uint32_t* seeds, void* stream);
+
+/* Environment.reset() (env.py:81-125) for env_ids[0..n) (device int32; NULL =
+ * all E envs, n ignored).  VectorizedEnv.reset(indices) (QMIX/env_vectorized.py:13-21).
+ * In MDL_TRACKER_FRESH mode the tracker is implicitly cleared; in
+ * MDL_TRACKER_MAPPO_STALE mode it is updated with the reset state, not cleared
+ * (MAPPO/trainer.py:232-233); mdl_tracker_clear() clears it explicitly. */
+int mdl_reset(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream);
+int mdl_tracker_clear(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream);
+
+/* One transition for env_ids[0..n) (NULL = all E in order).
+ * Environment.step (env.py:173-306) + compute_shaped_rewards
+ * (MAPPO/helper.py:257-369, evaluated with the pre-step tracker) + the
+ * tracker update (MAPPO/trainer.py:95-130) + optional reset-on-done
+ * (MAPPO/trainer.py:229-257).  actions: device uint8 [n][A] in
+ * `action_format`.  Outputs (device, [n], any may be NULL): r_env = the float
+ * reward env.step returns (fp64, bit-exact), r_shaped = the float32 value
+ * compute_shaped_rewards returns, done = check_terminate (env.py:308-316). */
+int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
+             int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
+
+/* Observation builders for envs [env_begin, env_begin+n), which must share one
+ * map shape (H, W), from the current state + tracker:
+ *   actor_map  f32 [n][A][6][H][W]          convert_observation       MAPPO/helper.py:6-66
+ *   actor_vec  f32 [n][A][6+5MO+5MP+1]      generate_vector_features  MAPPO/helper.py:68-165
+ *   critic_map f32 [n][4][H][W]             convert_global_state[0]   MAPPO/helper.py:167-198
+ *   critic_vec f32 [n][6MR+7MPs+1]          convert_global_state[1]   MAPPO/helper.py:199-255
+ * Any output pointer may be NULL. */
+int mdl_build_obs(MdlEngine* eng, int32_t env_begin, int32_t n, float* actor_map, float* actor_vec,
+                  float* critic_map, float* critic_vec, void* stream);
+
+/* State snapshot into caller DEVICE buffers (async on `stream`).  Any pointer may be NULL.
+ *   robots   int32 [E][A][3]  (row, col, carrying), 0-indexed
+ *   pkgs     int32 [E][P][8]  (sr, sc, tr, tc, start_time, deadline, id, status 0 None/1 waiting/2 in_transit/3 delivered)
+ *   t        int32 [E];  total_reward f64 [E]
+ *   tracker  int32 [E][P][4]  per id 1..P: (present, in_transit, order, _) ; data rows in tracker_data int32 [E][P][6]
+ * Backs the dict view of Environment.get_state (env.py:127-147). */
+int mdl_read_state(MdlEngine* eng, int32_t* robots, int32_t* pkgs, int32_t* t, double* total_reward,
+                   int32_t* tracker, int32_t* tracker_data, void* stream);
+
+/* Helper-compatible builders on arbitrary state dicts ("views"): the same
+ * device code as mdl_build_obs / the fused shaping, fed from a packed int32
+ * record per view instead of engine state.  View record layout (int32):
+ *   [0] t  [1] A  [2] n_slots  [3] map index
+ *   then A x (row, col, carrying)           0-indexed robot rows (state['robots'] minus 1)
+ *   then n_slots x (id, status 1|2, sr, sc, tr, tc, start_time, deadline)  tracker in dict order
+ * views: device int32 blob; offsets: device int64 [n_views] record starts;
+ * max_slots: the largest n_slots of any record (sizes the LDS slice).
+ * Robot and package cells must lie inside the view's map.
+ * agent_idx: device int32 [n_views] (may be out of range -> reference's
+ * early-return outputs).  Outputs per view: obs [6][H][W], vec [6+5MO+5MP+1],
+ * gmap [4][H][W], gvec [6MR+7MPs+1] (NULL to skip).  T/MO/MP/MR/MPs are call
+ * arguments here.  Replaces convert_observation / generate_vector_features /
+ * convert_global_state called on dicts (MAPPO/helper.py:6-255). */
+int mdl_views_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
+                       int32_t max_slots, const int32_t* agent_idx, int32_t T, int32_t MO, int32_t MP, int32_t MR, int32_t MPs,
+                       float* obs, float* vec, float* gmap, float* gvec, void* stream);
+
+/* compute_shaped_rewards (MAPPO/helper.py:257-369) on dict inputs: prev view
+ * record (state + tracker_prev as above), current robots int32 [A][3]
+ * (0-indexed) and time, actions uint8 [A] in MDL_ACTION_CODES, global reward
+ * (fp64).  cur: device int32 blob, cur_offsets: int64 [n] (record = [t, A,
+ * then A x 3]); actions: uint8 blob with act_offsets int64 [n]; g: f64 [n];
+ * consts: host double[9] (NULL = engine's).  Output: f32 [n]. */
+int mdl_views_shaped_reward(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets, int32_t max_slots,
+                            const int32_t* cur, const int64_t* cur_offsets, const uint8_t* actions,
+                            const int64_t* act_offsets, const double* g, int32_t n, const double* consts,
+                            float* out, void* stream);
+
+/* Host-only (no GPU needed): the distance-rank table the feature sorts use.
+ * out[(dr+H-1)*(2W-1) + dc+W-1] = rank of the fp64 key (dr/H)**2 + (dc/W)**2
+ * (CPython float_pow -> libm pow) among all distinct keys of the map shape;
+ * equal doubles share a rank.  out holds (2H-1)*(2W-1) entries.  This is the
+ * order of others.sort / pkgs.sort in MAPPO/helper.py:139,158. */
+int mdl_rank_table(int32_t H, int32_t W, uint16_t* out);
+
+/* Introspection */
+int mdl_get_config(const MdlEngine* eng, MdlConfig* out);
+int mdl_obs_dims(const MdlEngine* eng, int32_t* actor_vec_dim, int32_t* critic_vec_dim);
+const char* mdl_last_error(void);
+const char* mdl_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDL_ENGINE_H */

@@ -1,0 +1,408 @@
+// mdl_device.hpp -- device-side building blocks of the marl-delivery engine.
+//
+// Execution model (gfx950 / CDNA4): ONE WAVEFRONT (64 lanes) PER ENV INSTANCE.
+//   * robots live on lanes (lane a = robot a, A <= 64), so the cell-contention
+//     rule is resolved with readlane / ballot, no LDS round trips;
+//   * package tables are staged in the wave's slice of LDS and scanned with
+//     lanes over packages (64 per pass);
+//   * every sequential piece of the reference (reward fold in robot order,
+//     numpy RNG draws, numpy's pairwise float32 sum) runs as wave-uniform
+//     scalar code on values broadcast by readlane.
+// Waves of one workgroup are independent envs and never barrier together;
+// intra-wave LDS ordering uses wave_sync() (wavefront-scope fences).
+//
+// Reference semantics are cited path:line under the reference tree.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mdl {
+
+constexpr int WAVE = 64;
+constexpr int MT_N = 624;
+constexpr int MT_M = 397;
+constexpr int MAX_MAPS = 8;
+
+enum : int { ST_NONE = 0, ST_WAITING = 1, ST_IN_TRANSIT = 2, ST_DELIVERED = 3 };
+enum : int { MV_S = 0, MV_L = 1, MV_R = 2, MV_U = 3, MV_D = 4, MV_OTHER = 5 };
+// shaping constant slots (MAPPO/helper.py:271-279 order of use)
+enum : int { SH_PICK = 0, SH_ONTIME, SH_LATE, SH_CLOSER, SH_WPICK, SH_WDROP, SH_STUCK, SH_IDLE, SH_AWAY };
+
+struct MapDesc {
+    int H, W, nfree;
+    int grid_off;   // into grids (bytes)
+    int free_off;   // into free_cells (u16 packed r | c<<8, row-major)
+    int rank_off;   // into rank (u16) table [(2H-1)][(2W-1)]
+    float inv_hw;   // 1/(H*W) for fast divmod
+    int pad;
+};
+
+// Everything a kernel needs about the engine, passed by value.
+struct DevParams {
+    int E, A, P, T;
+    double move_cost, delivery_reward, delay_reward;
+    float shaping[9];
+    int stale;
+    int obsT, MO, MP, MR, MPs;
+    int n_maps;
+    MapDesc maps[MAX_MAPS];
+    const uint8_t* grids;
+    const uint16_t* free_cells;
+    const uint16_t* rank;
+    const uint8_t* env_map;   // [E] or null
+    // state (SoA, env-major)
+    uint16_t* rob;            // [E][A] r | c<<8
+    uint16_t* carry;          // [E][A]
+    uint64_t* pkg;            // [E][P] sr|sc<<8|tr<<16|tc<<24|st<<32|dl<<48
+    uint8_t* status;          // [E][P]
+    int32_t* t;               // [E]
+    double* total;            // [E]
+    uint32_t* mt;             // [E][624]
+    int32_t* mt_pos;          // [E]
+    uint8_t* trk_flag;        // [E][P] bit0 present, bit1 in_transit  (stale mode)
+    uint32_t* trk_seq;        // [E][P] insertion order                 (stale mode)
+    uint64_t* trk_pkg;        // [E][P] data copy at insertion          (stale mode)
+    uint32_t* trk_ctr;        // [E]
+    double* ep_total;         // [E] total_reward of the last finished episode
+    int32_t* ep_len;          // [E]
+};
+
+// ---------------------------------------------------------------- wave utils
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ int rdl(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ float rdlf(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
+__device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((long long)m) - 1; }
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    int l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// Correctly rounded int/int division in float32.  For |a|,|b| < 2^24 this
+// equals float32(double(a)/double(b)) (double rounding is innocuous for
+// division when 53 >= 2*24+2), i.e. what np.array([a/b], float32) stores.
+__device__ __forceinline__ float qdiv(int a, int b) { return (float)a / (float)b; }
+
+// i / d for 0 <= i < 2^23 using a float reciprocal and one correction.
+__device__ __forceinline__ int fdivi(int i, int d, float inv) {
+    int q = (int)((float)i * inv);
+    int r = i - q * d;
+    if (r < 0) q -= 1;
+    else if (r >= d) q += 1;
+    return q;
+}
+
+__device__ __forceinline__ int cell_r(int pc) { return pc & 255; }
+__device__ __forceinline__ int cell_c(int pc) { return (pc >> 8) & 255; }
+__device__ __forceinline__ int manhattan(int a, int b) {
+    return abs(cell_r(a) - cell_r(b)) + abs(cell_c(a) - cell_c(b));
+}
+
+__device__ __forceinline__ int pk_start(uint64_t v) { return (int)(v & 0xffff); }
+__device__ __forceinline__ int pk_target(uint64_t v) { return (int)((v >> 16) & 0xffff); }
+__device__ __forceinline__ int pk_st(uint64_t v) { return (int)((v >> 32) & 0xffff); }
+__device__ __forceinline__ int pk_dl(uint64_t v) { return (int)(v >> 48); }
+__device__ __forceinline__ uint64_t pk_make(int start, int target, int st, int dl) {
+    return (uint64_t)(uint32_t)start | ((uint64_t)(uint32_t)target << 16) | ((uint64_t)(uint32_t)st << 32) |
+           ((uint64_t)(uint32_t)dl << 48);
+}
+
+// Action decode.  MDL_ACTION_TRAINER_INT: MAPPO/trainer.py:198-205 with the
+// LabelEncoder class order D,L,R,S,U; MDL_ACTION_CODES: move | op<<3.
+__device__ __forceinline__ void decode_action(int a, int fmt, int& mv, int& op) {
+    if (fmt == 0) {
+        const int q = a / 5;
+        const int m = a - 5 * q;
+        // D,L,R,S,U -> codes 4,1,2,0,3
+        mv = (0x30214 >> (4 * m)) & 0xf;
+        op = q >= 3 ? 0 : q;
+    } else {
+        mv = a & 7;
+        op = (a >> 3) & 3;
+        if (mv > MV_OTHER) mv = MV_OTHER;
+    }
+}
+
+// ------------------------------------------------- numpy legacy RandomState
+// MT19937 state lives in the wave's LDS slice while a reset runs.
+// Twist: 64 lanes per round; round-ordered so reads of key[i+1] see old
+// values and reads of key[i-227] (i >= 227) see new ones, exactly as the
+// sequential mt19937_gen.
+__device__ inline void mt_twist(uint32_t* key) {
+    const int lane = lane_id();
+    for (int base = 0; base < MT_N; base += WAVE) {
+        const int i = base + lane;
+        uint32_t v = 0;
+        if (i < MT_N) {
+            const uint32_t y = (key[i] & 0x80000000u) | (key[i + 1 == MT_N ? 0 : i + 1] & 0x7fffffffu);
+            const int k = i + MT_M < MT_N ? i + MT_M : i + MT_M - MT_N;
+            v = key[k] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        wave_sync();
+        if (i < MT_N) key[i] = v;
+        wave_sync();
+    }
+}
+
+struct MTState {
+    uint32_t* key;  // LDS
+    int pos;        // wave-uniform
+};
+
+__device__ inline uint32_t mt_next32(MTState& s) {
+    if (s.pos == MT_N) {
+        mt_twist(s.key);
+        s.pos = 0;
+    }
+    uint32_t y = s.key[s.pos];
+    s.pos++;
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return (uint32_t)uni((int)y);
+}
+
+// RandomState.randint(lo, hi): hi exclusive; rng==0 -> lo with NO draw;
+// masked rejection on 32-bit draws (numpy distributions.c
+// buffered_bounded_masked_uint32).  Caller guarantees lo < hi.
+__device__ inline int randint(MTState& s, int lo, int hi) {
+    const uint32_t rng = (uint32_t)(hi - 1 - lo);
+    if (rng == 0) return lo;
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    do {
+        v = mt_next32(s) & mask;
+    } while (v > rng);
+    return lo + (int)v;
+}
+
+// ------------------------------------------------------------------ reset
+// Environment.reset() (env.py:81-125) for one env, wave-cooperative.
+// Writes robots (lane a: packed cell), the sorted package table into pk[]
+// (LDS) and initial statuses into pst[] (LDS).  scratch: LDS u64[P] + u16[64].
+struct ResetOut {
+    int robot_cell;   // lane a < A
+};
+
+__device__ inline int reset_env(MTState& mt, const DevParams& p, const MapDesc& md, uint64_t* pk, uint8_t* pst,
+                                uint64_t* scratch, uint16_t* taken) {
+    const int lane = lane_id();
+    const int A = p.A, P = p.P;
+    const uint16_t* fl = p.free_cells + md.free_off;
+    const int F = md.nfree;
+    // robots: get_random_free_cell(tmp_grid) env.py:161-170 -- the k-th
+    // not-yet-taken free cell in row-major order.
+    int my_cell = 0;
+    int ntk = 0;
+    for (int i = 0; i < A; i++) {
+        const int k = randint(mt, 0, F - i);
+        int idx = k;
+        for (int q = 0; q < ntk; q++) {
+            const int tq = taken[q];
+            if (tq <= idx) idx++;
+            else break;
+        }
+        // insert idx into the sorted taken list (one lane shifts)
+        if (lane == 0) {
+            int q = ntk;
+            while (q > 0 && taken[q - 1] > idx) {
+                taken[q] = taken[q - 1];
+                q--;
+            }
+            taken[q] = (uint16_t)idx;
+        }
+        ntk++;
+        wave_sync();
+        if (lane == i) my_cell = fl[idx];
+    }
+    // packages env.py:102-117 (draw order: start, target(s), deadline, start_time)
+    const int N = md.H;
+    const int lim = A < 20 ? A : 20;
+    for (int i = 0; i < P; i++) {
+        const int start = fl[randint(mt, 0, F)];
+        int target;
+        do {
+            target = fl[randint(mt, 0, F)];
+        } while (target == start);
+        const int to_dl = 10 + randint(mt, N / 2, 3 * N);
+        const int st = (i <= lim) ? 0 : randint(mt, 1, p.T);
+        if (lane == 0) scratch[i] = pk_make(start, target, st, st + to_dl);
+    }
+    wave_sync();
+    // stable sort by start_time (env.py:119): rank = #(st_i < st_j) + #(i < j, st_i == st_j)
+    for (int j0 = 0; j0 < P; j0 += WAVE) {
+        const int j = j0 + lane;
+        uint64_t v = 0;
+        int sj = 0, rank = 0;
+        if (j < P) {
+            v = scratch[j];
+            sj = pk_st(v);
+        }
+        for (int i = 0; i < P; i++) {
+            const int si = pk_st(scratch[i]);
+            rank += (si < sj) || (si == sj && i < j);
+        }
+        if (j < P) {
+            pk[rank] = v;
+        }
+    }
+    wave_sync();
+    for (int j = lane; j < P; j += WAVE) pst[j] = pk_st(pk[j]) == 0 ? ST_WAITING : ST_NONE;  // get_state at t=0
+    wave_sync();
+    return my_cell;
+}
+
+// ------------------------------------------------------- tracker accessors
+// The persistent-package dict (MAPPO/trainer.py:95-130) seen through one
+// interface: slot j -> present / in_transit / start / target / start_time /
+// deadline / id / iteration order.
+struct TrkFresh {  // == env truth: ids in spawn (= id) order
+    const uint64_t* pk;
+    const uint8_t* st;
+    int n;
+    __device__ int count() const { return n; }
+    __device__ bool present(int j) const { const int s = st[j]; return s == ST_WAITING || s == ST_IN_TRANSIT; }
+    __device__ bool in_transit(int j) const { return st[j] == ST_IN_TRANSIT; }
+    __device__ uint64_t data(int j) const { return pk[j]; }
+    __device__ int id(int j) const { return j + 1; }
+    __device__ uint32_t order(int j) const { return (uint32_t)j; }
+    __device__ int slot_of(int id) const { return (id >= 1 && id <= n && present(id - 1)) ? id - 1 : -1; }
+};
+
+struct TrkStale {  // explicit per-id slots (never cleared on auto-reset)
+    const uint8_t* flag;
+    const uint32_t* seq;
+    const uint64_t* pk;
+    int n;
+    __device__ int count() const { return n; }
+    __device__ bool present(int j) const { return flag[j] & 1; }
+    __device__ bool in_transit(int j) const { return (flag[j] & 2) != 0; }
+    __device__ uint64_t data(int j) const { return pk[j]; }
+    __device__ int id(int j) const { return j + 1; }
+    __device__ uint32_t order(int j) const { return seq[j]; }
+    __device__ int slot_of(int id) const { return (id >= 1 && id <= n && present(id - 1)) ? id - 1 : -1; }
+};
+
+struct TrkView {  // arbitrary dict from a packed view record (dict order)
+    const int32_t* ids;
+    const uint8_t* flag;
+    const uint64_t* pk;
+    int n;
+    __device__ int count() const { return n; }
+    __device__ bool present(int j) const { return flag[j] & 1; }
+    __device__ bool in_transit(int j) const { return (flag[j] & 2) != 0; }
+    __device__ uint64_t data(int j) const { return pk[j]; }
+    __device__ int id(int j) const { return ids[j]; }
+    __device__ uint32_t order(int j) const { return (uint32_t)j; }
+    __device__ int slot_of(int id) const {
+        for (int j = 0; j < n; j++)
+            if (ids[j] == id) return j;
+        return -1;
+    }
+};
+
+// ----------------------------------------------------------- shaped reward
+// compute_shaped_rewards (MAPPO/helper.py:257-369) for the agent on this lane.
+// float32 accumulation in the reference's order (NEP 50: each constant is
+// rounded to float32 first).  Returns this lane's shaped_rewards[a].
+template <class Trk>
+__device__ inline float shaped_agent(const Trk& trk, const float* C, bool active, int prev_cell, int prev_carry,
+                                     int cur_cell, int cur_carry, int mv, int op, int t_prev, int t_cur) {
+    float s = 0.0f;
+    const int pslot = (active && prev_carry != 0) ? trk.slot_of(prev_carry) : -1;
+    // 1. pickup / delivery
+    if (prev_carry == 0 && cur_carry != 0) {
+        s = s + C[SH_PICK];
+    } else if (prev_carry != 0 && cur_carry == 0) {
+        if (pslot >= 0) {
+            const uint64_t d = trk.data(pslot);
+            if (cur_cell == pk_target(d)) s = s + ((t_cur <= pk_dl(d)) ? C[SH_ONTIME] : C[SH_LATE]);
+        }
+    }
+    const bool moved = prev_cell != cur_cell;
+    // scan of waiting (st <= t_prev) entries: can_pickup / nearest / idle
+    const bool need_can = active && op == 1 && prev_carry == 0 && cur_carry == 0;
+    const bool need_near = active && moved && !(prev_carry != 0 && pslot >= 0);
+    const bool need_idle = active && !moved && mv == MV_S && prev_carry == 0;
+    bool can = false, idle = false;
+    int best_d = 0x7fffffff;
+    uint32_t best_o = 0xffffffffu;
+    int best_cell = -1;
+    if (__ballot(need_can || need_near || need_idle)) {
+        const int n = trk.count();
+        for (int j = 0; j < n; j++) {
+            if (!trk.present(j) || trk.in_transit(j)) continue;
+            const uint64_t d = trk.data(j);
+            if (pk_st(d) > t_prev) continue;
+            const int sc = pk_start(d);
+            can |= sc == cur_cell;
+            const int md = manhattan(prev_cell, sc);
+            idle |= md <= 3;
+            const uint32_t o = trk.order(j);
+            if (md < best_d || (md == best_d && o < best_o)) {
+                best_d = md;
+                best_o = o;
+                best_cell = sc;
+            }
+        }
+    }
+    // 2. wasted operations
+    if (op == 1) {
+        if (prev_carry != 0) s = s + C[SH_WPICK];
+        else if (cur_carry == 0 && !can) s = s + C[SH_WPICK];
+    } else if (op == 2) {
+        if (prev_carry == 0) s = s + C[SH_WDROP];
+        else if (cur_carry != 0 && pslot >= 0 && cur_cell != pk_target(trk.data(pslot))) s = s + C[SH_WDROP];
+    }
+    // 3. movement
+    if (mv != MV_S && !moved) s = s + C[SH_STUCK];
+    int target = -1;
+    if (prev_carry != 0 && pslot >= 0) target = pk_target(trk.data(pslot));
+    else target = best_cell;
+    if (target >= 0 && moved) {
+        const int db = manhattan(prev_cell, target), da = manhattan(cur_cell, target);
+        if (da < db) s = s + C[SH_CLOSER];
+        else if (da > db) s = s + C[SH_AWAY];
+    }
+    // 4. idle near an available package
+    if (!moved && mv == MV_S && prev_carry == 0 && idle) s = s + C[SH_IDLE];
+    return active ? s : 0.0f;
+}
+
+// numpy float32 add.reduce over lanes 0..n-1 (n <= 64): 0 + pairwise_sum
+// (8 running partials for n >= 8, sequential tail).  Wave-uniform result.
+__device__ inline float np_sum_lanes(float v, int n) {
+    float res;
+    if (n < 8) {
+        res = 0.0f;
+        for (int i = 0; i < n; i++) res = res + rdlf(v, i);
+    } else {
+        float r0 = rdlf(v, 0), r1 = rdlf(v, 1), r2 = rdlf(v, 2), r3 = rdlf(v, 3);
+        float r4 = rdlf(v, 4), r5 = rdlf(v, 5), r6 = rdlf(v, 6), r7 = rdlf(v, 7);
+        int i;
+        for (i = 8; i < n - (n % 8); i += 8) {
+            r0 = r0 + rdlf(v, i + 0); r1 = r1 + rdlf(v, i + 1); r2 = r2 + rdlf(v, i + 2); r3 = r3 + rdlf(v, i + 3);
+            r4 = r4 + rdlf(v, i + 4); r5 = r5 + rdlf(v, i + 5); r6 = r6 + rdlf(v, i + 6); r7 = r7 + rdlf(v, i + 7);
+        }
+        res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        for (; i < n; i++) res = res + rdlf(v, i);
+    }
+    return 0.0f + res;
+}
+
+}  // namespace mdl

@@ -1,0 +1,421 @@
+// mdl_engine.hip -- host side of the C ABI declared in include/mdl_engine.h.
+//
+// Owns the engine's SoA state in HBM (hipMalloc), validates configurations the
+// reference would reject (or loop forever on), builds the per-map tables
+// (row-major free-cell lists for the reset draws, fp64 distance-rank tables
+// for the feature sorts) and launches the kernels of mdl_kernels.hip.
+#include "mdl_engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mdl_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return -1;
+}
+
+#define HIPCHK(x)                                                                       \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) return fail("%s failed: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr size_t LDS_BUDGET = 64 * 1024;  // dynamic LDS per 256-thread workgroup
+
+// CPython float_pow(x, 2.0) -> libm pow(|x|, 2.0) (special cases 0 and 1).
+// Called through a volatile pointer so the compiler cannot fold it to x*x:
+// the reference's sort keys are exactly these doubles (MAPPO/helper.py:139,158).
+double (*volatile g_pow)(double, double) = pow;
+double py_sq(double x) {
+    if (x == 0.0) return 0.0;
+    if (x < 0) x = -x;
+    if (x == 1.0) return 1.0;
+    return g_pow(x, 2.0);
+}
+
+// rank[(dr+H-1)*(2W-1) + dc+W-1] = rank of (dr/H)**2 + (dc/W)**2 among all
+// distinct values (equal doubles share a rank).
+void build_rank(int H, int W, std::vector<uint16_t>& out) {
+    const int R = 2 * H - 1, C = 2 * W - 1;
+    std::vector<double> key((size_t)R * C);
+    for (int dr = -(H - 1); dr <= H - 1; dr++)
+        for (int dc = -(W - 1); dc <= W - 1; dc++)
+            key[(size_t)(dr + H - 1) * C + (dc + W - 1)] = py_sq((double)dr / (double)H) + py_sq((double)dc / (double)W);
+    std::vector<double> u = key;
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    out.resize(key.size());
+    for (size_t i = 0; i < key.size(); i++)
+        out[i] = (uint16_t)(std::lower_bound(u.begin(), u.end(), key[i]) - u.begin());
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int waves_per_block(size_t lds_per_wave) {
+    if (lds_per_wave == 0) return 4;
+    size_t w = LDS_BUDGET / lds_per_wave;
+    if (w > 4) w = 4;
+    return (int)w;
+}
+
+}  // namespace
+
+struct MdlEngine {
+    MdlConfig cfg{};
+    int device = 0;
+    mdl::DevParams p{};
+    std::vector<int> mapH, mapW;
+    std::vector<void*> allocs;
+    size_t lds_step = 0, lds_obs = 0;
+    int wpb_step = 1, wpb_obs = 1;
+    int maxHW = 0;
+    bool seeded = false;
+
+    template <class T>
+    int alloc(T** ptr, size_t count) {
+        void* v = nullptr;
+        const size_t bytes = count * sizeof(T) > 0 ? count * sizeof(T) : 16;
+        hipError_t e = hipMalloc(&v, bytes);
+        if (e != hipSuccess) return fail("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        allocs.push_back(v);
+        e = hipMemset(v, 0, bytes);
+        if (e != hipSuccess) return fail("hipMemset failed: %s", hipGetErrorString(e));
+        *ptr = (T*)v;
+        return 0;
+    }
+    ~MdlEngine() {
+        for (void* v : allocs) (void)hipFree(v);
+    }
+};
+
+extern "C" {
+
+const char* mdl_last_error(void) { return g_err.c_str(); }
+const char* mdl_version(void) { return "mdl-engine 0.1 gfx950"; }
+
+int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw, int32_t n_maps,
+               const int32_t* env_map, int32_t device, MdlEngine** out) {
+    if (!cfg || !grids || !map_hw || !out) return fail("mdl_create: null argument");
+    *out = nullptr;
+    const MdlConfig& c = *cfg;
+    if (c.n_envs < 1) return fail("n_envs must be >= 1");
+    if (c.n_robots < 1 || c.n_robots > MDL_MAX_ROBOTS) return fail("n_robots must be in [1, %d]", MDL_MAX_ROBOTS);
+    if (c.n_packages < 1 || c.n_packages > MDL_MAX_PACKAGES)
+        return fail("n_packages must be in [1, %d]", MDL_MAX_PACKAGES);
+    if (c.max_time_steps < 1) return fail("max_time_steps must be >= 1");
+    if (n_maps < 1 || n_maps > mdl::MAX_MAPS) return fail("n_maps must be in [1, %d]", mdl::MAX_MAPS);
+    if (c.tracker_mode != MDL_TRACKER_FRESH && c.tracker_mode != MDL_TRACKER_MAPPO_STALE)
+        return fail("unknown tracker_mode %d", c.tracker_mode);
+    if (c.max_other_robots < 0 || c.max_packages_obs < 0 || c.max_robots_state < 0 || c.max_packages_state < 0)
+        return fail("observation slot counts must be >= 0");
+    // env.py:113-116: start_time = randint(1, T) for packages beyond min(A,20)+1 -> needs T >= 2
+    const int lim = c.n_robots < 20 ? c.n_robots : 20;
+    if (c.n_packages > lim + 1 && c.max_time_steps < 2)
+        return fail("max_time_steps must be >= 2 when n_packages > min(n_robots,20)+1 (numpy randint(1, T))");
+
+    MdlEngine* eng = new MdlEngine();
+    eng->cfg = c;
+    eng->device = device;
+    DeviceGuard dg(device);
+    if (!dg.ok) {
+        delete eng;
+        return fail("hipSetDevice(%d) failed", device);
+    }
+
+    // ---- maps ----
+    std::vector<uint8_t> allgrid;
+    std::vector<uint16_t> allfree, allrank;
+    mdl::DevParams& p = eng->p;
+    size_t goff = 0;
+    for (int m = 0; m < n_maps; m++) {
+        const int H = map_hw[2 * m], W = map_hw[2 * m + 1];
+        if (H < 1 || W < 1 || H > 255 || W > 255 || H * W > MDL_MAX_CELLS) {
+            delete eng;
+            return fail("map %d: H, W must be in [1,255] with H*W <= %d", m, MDL_MAX_CELLS);
+        }
+        const uint8_t* g = grids + goff;
+        mdl::MapDesc& md = p.maps[m];
+        md.H = H;
+        md.W = W;
+        md.grid_off = (int)allgrid.size();
+        md.free_off = (int)allfree.size();
+        md.rank_off = (int)allrank.size();
+        md.inv_hw = 1.0f / (float)(H * W);
+        int nf = 0;
+        for (int i = 0; i < H * W; i++) {
+            if (g[i] > 1) {
+                delete eng;
+                return fail("map %d: cells must be 0 or 1", m);
+            }
+            allgrid.push_back(g[i]);
+            if (g[i] == 0) {
+                allfree.push_back((uint16_t)((i / W) | ((i % W) << 8)));
+                nf++;
+            }
+        }
+        md.nfree = nf;
+        if (nf < c.n_robots) {
+            delete eng;
+            return fail("map %d has %d free cells < n_robots %d (numpy randint(0, 0) raises)", m, nf, c.n_robots);
+        }
+        if (nf < 2) {
+            delete eng;
+            return fail("map %d needs >= 2 free cells (start != target loop, env.py:107-111)", m);
+        }
+        if ((long)c.max_time_steps - 1 + 10 + 3L * H > 65535) {
+            delete eng;
+            return fail("deadlines must fit 16 bits (T + 3H + 9 <= 65535)");
+        }
+        std::vector<uint16_t> rk;
+        build_rank(H, W, rk);
+        allrank.insert(allrank.end(), rk.begin(), rk.end());
+        eng->mapH.push_back(H);
+        eng->mapW.push_back(W);
+        eng->maxHW = std::max(eng->maxHW, H * W);
+        goff += (size_t)H * W;
+    }
+    std::vector<uint8_t> em;
+    if (env_map) {
+        em.resize(c.n_envs);
+        for (int e = 0; e < c.n_envs; e++) {
+            if (env_map[e] < 0 || env_map[e] >= n_maps) {
+                delete eng;
+                return fail("env_map[%d] = %d out of range", e, env_map[e]);
+            }
+            em[e] = (uint8_t)env_map[e];
+        }
+    }
+
+    p.E = c.n_envs;
+    p.A = c.n_robots;
+    p.P = c.n_packages;
+    p.T = c.max_time_steps;
+    p.move_cost = c.move_cost;
+    p.delivery_reward = c.delivery_reward;
+    p.delay_reward = c.delay_reward;
+    for (int i = 0; i < 9; i++) p.shaping[i] = (float)c.shaping[i];  // NEP 50: constants rounded to float32
+    p.stale = c.tracker_mode == MDL_TRACKER_MAPPO_STALE;
+    p.obsT = c.obs_max_time_steps;
+    p.MO = c.max_other_robots;
+    p.MP = c.max_packages_obs;
+    p.MR = c.max_robots_state;
+    p.MPs = c.max_packages_state;
+    p.n_maps = n_maps;
+
+    const size_t E = c.n_envs, A = c.n_robots, P = c.n_packages;
+    uint8_t* d_grid = nullptr;
+    uint16_t *d_free = nullptr, *d_rank = nullptr;
+    uint8_t* d_em = nullptr;
+    int rc = 0;
+    rc |= eng->alloc(&d_grid, allgrid.size());
+    rc |= eng->alloc(&d_free, allfree.size());
+    rc |= eng->alloc(&d_rank, allrank.size());
+    if (env_map) rc |= eng->alloc(&d_em, E);
+    rc |= eng->alloc(&p.rob, E * A);
+    rc |= eng->alloc(&p.carry, E * A);
+    rc |= eng->alloc(&p.pkg, E * P);
+    rc |= eng->alloc(&p.status, E * P);
+    rc |= eng->alloc(&p.t, E);
+    rc |= eng->alloc(&p.total, E);
+    rc |= eng->alloc(&p.mt, E * mdl::MT_N);
+    rc |= eng->alloc(&p.mt_pos, E);
+    const size_t tE = p.stale ? E : 1;
+    rc |= eng->alloc(&p.trk_flag, tE * P);
+    rc |= eng->alloc(&p.trk_seq, tE * P);
+    rc |= eng->alloc(&p.trk_pkg, tE * P);
+    rc |= eng->alloc(&p.trk_ctr, tE);
+    rc |= eng->alloc(&p.ep_total, E);
+    rc |= eng->alloc(&p.ep_len, E);
+    if (rc) {
+        std::string msg = g_err;
+        delete eng;
+        return fail("%s", msg.c_str());
+    }
+    if (hipMemcpy(d_grid, allgrid.data(), allgrid.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_free, allfree.data(), allfree.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_rank, allrank.data(), allrank.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+        (env_map && hipMemcpy(d_em, em.data(), E, hipMemcpyHostToDevice) != hipSuccess)) {
+        delete eng;
+        return fail("hipMemcpy of map tables failed");
+    }
+    p.grids = d_grid;
+    p.free_cells = d_free;
+    p.rank = d_rank;
+    p.env_map = d_em;
+
+    eng->lds_step = mdl::step_lds((int)P);
+    eng->wpb_step = waves_per_block(eng->lds_step);
+    eng->lds_obs = mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MP, p.MPs);
+    eng->wpb_obs = waves_per_block(eng->lds_obs);
+    if (eng->wpb_step < 1 || eng->wpb_obs < 1) {
+        delete eng;
+        return fail("configuration needs more than %zu bytes of LDS per env", LDS_BUDGET);
+    }
+    *out = eng;
+    return 0;
+}
+
+int mdl_destroy(MdlEngine* eng) {
+    if (!eng) return 0;
+    DeviceGuard dg(eng->device);
+    (void)hipDeviceSynchronize();
+    delete eng;
+    return 0;
+}
+
+int mdl_seed(MdlEngine* eng, const uint32_t* seeds, void* stream) {
+    if (!eng || !seeds) return fail("mdl_seed: null argument");
+    DeviceGuard dg(eng->device);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t* d = nullptr;
+    const size_t bytes = sizeof(uint32_t) * eng->p.E;
+    HIPCHK(hipMalloc(&d, bytes));
+    hipError_t e = hipMemcpyAsync(d, seeds, bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = mdl::launch_seed(eng->p, d, eng->wpb_step, eng->lds_step, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail("mdl_seed: %s", hipGetErrorString(e));
+    eng->seeded = true;
+    return 0;
+}
+
+int mdl_reset(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream) {
+    if (!eng) return fail("mdl_reset: null engine");
+    if (!eng->seeded) return fail("mdl_reset: engine not seeded (call mdl_seed first)");
+    if (!env_ids) n = eng->p.E;
+    if (n < 0 || n > eng->p.E) return fail("mdl_reset: n=%d out of range", n);
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_reset(eng->p, env_ids, n, eng->wpb_step, eng->lds_step, (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_tracker_clear(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream) {
+    if (!eng) return fail("mdl_tracker_clear: null engine");
+    if (!eng->p.stale) return 0;  // fresh tracker has no storage
+    if (!env_ids) n = eng->p.E;
+    if (n < 0 || n > eng->p.E) return fail("mdl_tracker_clear: n=%d out of range", n);
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_tracker_clear(eng->p, env_ids, n, (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
+             int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream) {
+    if (!eng || !actions) return fail("mdl_step: null argument");
+    if (!eng->seeded) return fail("mdl_step: engine not seeded (call mdl_seed first)");
+    if (action_format != MDL_ACTION_TRAINER_INT && action_format != MDL_ACTION_CODES)
+        return fail("mdl_step: unknown action_format %d", action_format);
+    if (!env_ids) n = eng->p.E;
+    if (n < 0 || n > eng->p.E) return fail("mdl_step: n=%d out of range", n);
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_step(eng->p, actions, action_format, env_ids, n, auto_reset, r_env, r_shaped, done,
+                            eng->wpb_step, eng->lds_step, (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_build_obs(MdlEngine* eng, int32_t env_begin, int32_t n, float* actor_map, float* actor_vec,
+                  float* critic_map, float* critic_vec, void* stream) {
+    if (!eng) return fail("mdl_build_obs: null engine");
+    if (env_begin < 0 || n < 0 || env_begin + n > eng->p.E) return fail("mdl_build_obs: env range out of bounds");
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_obs(eng->p, env_begin, n, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs,
+                           eng->lds_obs, (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_read_state(MdlEngine* eng, int32_t* robots, int32_t* pkgs, int32_t* t, double* total_reward,
+                   int32_t* tracker, int32_t* tracker_data, void* stream) {
+    if (!eng) return fail("mdl_read_state: null engine");
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_export(eng->p, robots, pkgs, t, total_reward, tracker, tracker_data, (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_views_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
+                       int32_t max_slots, const int32_t* agent_idx, int32_t T, int32_t MO, int32_t MP, int32_t MR,
+                       int32_t MPs, float* obs, float* vec, float* gmap, float* gvec, void* stream) {
+    if (!eng || !views || !offsets) return fail("mdl_views_features: null argument");
+    if (n_views < 0 || max_slots < 0 || max_slots > 4096) return fail("mdl_views_features: bad sizes");
+    if (MO < 0 || MP < 0 || MR < 0 || MPs < 0) return fail("mdl_views_features: negative slot count");
+    if (n_views == 0) return 0;
+    const int MPc = std::min(MP, max_slots), MPsc = std::min(MPs, max_slots);
+    const size_t lds = mdl::views_lds(max_slots, eng->maxHW, MPc, MPsc);
+    const int wpb = waves_per_block(lds);
+    if (wpb < 1) return fail("mdl_views_features: needs %zu bytes of LDS per view", lds);
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_views_features(eng->p, views, offsets, n_views, agent_idx, T, MO, MP, MR, MPs, MPc, MPsc,
+                                      max_slots, eng->maxHW, obs, vec, gmap, gvec, wpb, lds, (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_views_shaped_reward(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets,
+                            int32_t max_slots, const int32_t* cur, const int64_t* cur_offsets, const uint8_t* actions,
+                            const int64_t* act_offsets, const double* g, int32_t n, const double* consts, float* out,
+                            void* stream) {
+    if (!eng || !prev_views || !prev_offsets || !cur || !cur_offsets || !actions || !act_offsets || !g || !out)
+        return fail("mdl_views_shaped_reward: null argument");
+    if (n < 0 || max_slots < 0 || max_slots > 4096) return fail("mdl_views_shaped_reward: bad sizes");
+    if (n == 0) return 0;
+    mdl::ShapingConsts C;
+    for (int i = 0; i < 9; i++) C.c[i] = consts ? (float)consts[i] : eng->p.shaping[i];
+    const size_t lds = mdl::views_shaped_lds(max_slots);
+    const int wpb = waves_per_block(lds);
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_views_shaped(eng->p, prev_views, prev_offsets, cur, cur_offsets, actions, act_offsets, g, n, C,
+                                    out, wpb, lds, max_slots, (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_rank_table(int32_t H, int32_t W, uint16_t* out) {
+    if (!out || H < 1 || W < 1 || H > 255 || W > 255) return fail("mdl_rank_table: bad arguments");
+    std::vector<uint16_t> rk;
+    build_rank(H, W, rk);
+    std::memcpy(out, rk.data(), rk.size() * sizeof(uint16_t));
+    return 0;
+}
+
+int mdl_get_config(const MdlEngine* eng, MdlConfig* out) {
+    if (!eng || !out) return fail("mdl_get_config: null argument");
+    *out = eng->cfg;
+    return 0;
+}
+
+int mdl_obs_dims(const MdlEngine* eng, int32_t* actor_vec_dim, int32_t* critic_vec_dim) {
+    if (!eng) return fail("mdl_obs_dims: null engine");
+    if (actor_vec_dim) *actor_vec_dim = 6 + 5 * eng->p.MO + 5 * eng->p.MP + 1;
+    if (critic_vec_dim) *critic_vec_dim = 6 * eng->p.MR + 7 * eng->p.MPs + 1;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,34 @@
+// mdl_kernels.hpp -- host-visible launchers of the gfx950 kernels (mdl_kernels.hip).
+#pragma once
+#include "mdl_device.hpp"
+
+namespace mdl {
+
+struct ShapingConsts {
+    float c[9];
+};
+
+hipError_t launch_seed(const DevParams& p, const uint32_t* seeds, int wpb, size_t lds, hipStream_t s);
+hipError_t launch_reset(const DevParams& p, const int* ids, int n, int wpb, size_t lds, hipStream_t s);
+hipError_t launch_tracker_clear(const DevParams& p, const int* ids, int n, hipStream_t s);
+hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
+                       double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s);
+hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
+                      int wpb, size_t lds, hipStream_t s);
+hipError_t launch_views_features(const DevParams& p, const int32_t* views, const int64_t* offs, int n,
+                                 const int32_t* agent_idx, int T, int MO, int MP, int MR, int MPs, int MPc, int MPsc,
+                                 int NSmax, int HW, float* obs, float* vec, float* gmap, float* gvec, int wpb,
+                                 size_t lds, hipStream_t s);
+hipError_t launch_views_shaped(const DevParams& p, const int32_t* prev, const int64_t* prev_offs, const int32_t* cur,
+                               const int64_t* cur_offs, const uint8_t* acts, const int64_t* act_offs, const double* g,
+                               int n, const ShapingConsts& C, float* out, int wpb, size_t lds, int NSmax,
+                               hipStream_t s);
+hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int32_t* t, double* total,
+                         int32_t* tracker, int32_t* tracker_data, hipStream_t s);
+
+size_t step_lds(int P);
+size_t obs_lds(int A, int P, int HW, int MP, int MPs);
+size_t views_lds(int NSmax, int HW, int MPc, int MPsc);
+size_t views_shaped_lds(int NSmax);
+
+}  // namespace mdl

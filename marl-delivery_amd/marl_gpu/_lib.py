@@ -1,0 +1,107 @@
+"""ctypes binding of the engine's C ABI (include/mdl_engine.h -> marl_gpu/libmdl.so).
+
+torch is imported first on purpose: torch bundles a HIP runtime whose SONAME
+(libamdhip64.so.7) equals the system one, so once torch is loaded the dynamic
+linker resolves libmdl.so's HIP imports to torch's runtime and device pointers
+and stream handles are shared between the two.
+
+There is no fallback: if the shared library is missing or fails to load, the
+import raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede loading libmdl.so, see module docstring)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmdl.so")
+
+MDL_TRACKER_FRESH = 0
+MDL_TRACKER_MAPPO_STALE = 1
+MDL_ACTION_TRAINER_INT = 0
+MDL_ACTION_CODES = 1
+MDL_MAX_ROBOTS = 64
+MDL_MAX_PACKAGES = 1024
+
+
+class MdlConfig(C.Structure):
+    _fields_ = [
+        ("n_envs", C.c_int32),
+        ("n_robots", C.c_int32),
+        ("n_packages", C.c_int32),
+        ("max_time_steps", C.c_int32),
+        ("move_cost", C.c_double),
+        ("delivery_reward", C.c_double),
+        ("delay_reward", C.c_double),
+        ("tracker_mode", C.c_int32),
+        ("shaping", C.c_double * 9),
+        ("obs_max_time_steps", C.c_int32),
+        ("max_other_robots", C.c_int32),
+        ("max_packages_obs", C.c_int32),
+        ("max_robots_state", C.c_int32),
+        ("max_packages_state", C.c_int32),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/mdl_engine.h declares
+_vp, _i32, _i64p = C.c_void_p, C.c_int32, C.c_void_p
+SIGNATURES = {
+    "mdl_create": (C.c_int, [C.POINTER(MdlConfig), _vp, _vp, _i32, _vp, _i32, C.POINTER(C.c_void_p)]),
+    "mdl_destroy": (C.c_int, [_vp]),
+    "mdl_seed": (C.c_int, [_vp, _vp, _vp]),
+    "mdl_reset": (C.c_int, [_vp, _vp, _i32, _vp]),
+    "mdl_tracker_clear": (C.c_int, [_vp, _vp, _i32, _vp]),
+    "mdl_step": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "mdl_build_obs": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "mdl_read_state": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mdl_views_features": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32,
+                                     _vp, _vp, _vp, _vp, _vp]),
+    "mdl_views_shaped_reward": (C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "mdl_rank_table": (C.c_int, [_i32, _i32, _vp]),
+    "mdl_get_config": (C.c_int, [_vp, C.POINTER(MdlConfig)]),
+    "mdl_obs_dims": (C.c_int, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "mdl_last_error": (C.c_char_p, []),
+    "mdl_version": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+class MdlError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmdl.so (raises if it is missing: the engine has no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"marl_gpu: {LIB_PATH} not built; run `make -C marl-delivery_amd` "
+                              "(or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().mdl_last_error().decode(errors="replace")
+        raise MdlError(f"{what}: {msg}" if what else msg)
+
+
+def ptr(t) -> int | None:
+    """Device (or host) address of a tensor / None."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,246 @@
+"""Drop-in dict API over the GPU engine.
+
+``Environment`` mirrors env.py:18-455 (constructor signature, attributes,
+``reset()`` / ``step()`` / ``get_state()`` dicts, ``render()``) and
+``VectorizedEnv`` mirrors MAPPO/env_vectorized.py:1-24 plus the ``indices=``
+variant of QMIX/env_vectorized.py:1-49, so agents and trainer loops written
+against the reference run unchanged.  Every transition executes on the GPU;
+the dicts are materialised from a device snapshot after each call.
+
+Differences (documented, not silent):
+  * ``step`` returns the int ``0`` whenever the step reward is 0.0 (the
+    reference returns the int 0 when no reward term fired, and a float that
+    happens to equal 0.0 in the rare case the terms cancel);
+  * ``render_pygame`` is a no-op (headless), ``render`` prints text as the
+    reference's ``render``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .engine import STATUS_NAMES, BatchedEnv
+from .maps import grid_array, load_map, map_path
+
+MOVE_CODES = {"S": 0, "L": 1, "R": 2, "U": 3, "D": 4}   # anything else -> 5 (no move, != 'S')
+OP_CODES = {"0": 0, "1": 1, "2": 2}                     # anything else -> 3 (no env effect)
+
+
+def encode_actions(actions, n_robots):
+    """list[(move_str, op_str)] -> packed codes (move | op << 3), env.py:193-195 strings."""
+    if len(actions) != n_robots:
+        raise ValueError("The number of actions must match the number of robots.")
+    out = np.empty(n_robots, np.uint8)
+    for i, (mv, op) in enumerate(actions):
+        m = MOVE_CODES.get(mv, 5)
+        out[i] = m | (OP_CODES.get(op, 3) << 3)
+    return out
+
+
+class Robot:
+    __slots__ = ("position", "carrying")
+
+    def __init__(self, position, carrying=0):
+        self.position = position
+        self.carrying = carrying
+
+
+class Package:
+    __slots__ = ("start", "start_time", "target", "deadline", "package_id", "status")
+
+    def __init__(self, start, start_time, target, deadline, package_id, status="None"):
+        self.start = start
+        self.start_time = start_time
+        self.target = target
+        self.deadline = deadline
+        self.package_id = package_id
+        self.status = status
+
+
+class _Slot:
+    """Host mirror of one env slot of a BatchedEnv, refreshed after each call."""
+
+    def __init__(self, owner, idx):
+        self._owner = owner
+        self._idx = idx
+
+    def _refresh(self, snap):
+        e = self._idx
+        rob = snap["robots"][e]
+        pk = snap["pkgs"][e]
+        self.t = int(snap["t"][e])
+        self.total_reward = float(snap["total_reward"][e])
+        self.robots = [Robot((int(r[0]), int(r[1])), int(r[2])) for r in rob]
+        self.packages = [Package((int(p[0]), int(p[1])), int(p[4]), (int(p[2]), int(p[3])), int(p[5]), int(p[6]),
+                                 STATUS_NAMES[int(p[7])]) for p in pk]
+
+    def _state_dict(self):
+        return {
+            "time_step": self.t,
+            "map": self.grid,
+            "robots": [(r.position[0] + 1, r.position[1] + 1, r.carrying) for r in self.robots],
+            "packages": [(p.package_id, p.start[0] + 1, p.start[1] + 1, p.target[0] + 1, p.target[1] + 1,
+                          p.start_time, p.deadline) for p in self.packages if p.start_time == self.t],
+        }
+
+
+class Environment(_Slot):
+    """env.py:18-455 on the GPU engine (one env)."""
+
+    def __init__(self, map_file, max_time_steps=100, n_robots=5, n_packages=20, move_cost=-0.01,
+                 delivery_reward=10., delay_reward=1., seed=2025, _engine=None, _idx=0):
+        self.map_file = map_file
+        self.grid = load_map(map_path(map_file)) if _engine is None else _engine._grid_list
+        self.n_rows = len(self.grid)
+        self.n_cols = len(self.grid[0]) if self.grid else 0
+        self.move_cost = move_cost
+        self.delivery_reward = delivery_reward
+        self.delay_reward = delay_reward
+        self.n_robots = n_robots
+        self.max_time_steps = max_time_steps
+        self.n_packages = n_packages
+        if _engine is None:
+            _engine = BatchedEnv(grid_array(self.grid), 1, n_robots, n_packages, max_time_steps, move_cost,
+                                 delivery_reward, delay_reward, seeds=[seed], tracker="fresh")
+            _engine._grid_list = self.grid
+            self._vec = None
+        super().__init__(_engine, _idx)
+        self.engine = _engine
+        self.done = False
+        self.state = None
+        if getattr(_engine, "_snap", None) is None:
+            _engine._snap = _snapshot(_engine)
+        self._refresh(_engine._snap)
+
+    # env.py:81-125
+    def reset(self):
+        ids = None if self.engine.E == 1 else [self._idx]
+        self.engine.reset(ids)
+        snap = _snapshot(self.engine)
+        self.engine._snap = snap
+        self._refresh(snap)
+        self.done = False
+        self.state = None
+        return self._state_dict()
+
+    def get_state(self):
+        return self._state_dict()
+
+    # env.py:173-306
+    def step(self, actions):
+        codes = encode_actions(actions, self.n_robots)
+        eng = self.engine
+        a = torch.from_numpy(codes).to(eng.device).view(1, -1)
+        ids = None if eng.E == 1 else [self._idx]
+        r, _, d = eng.step(a, env_ids=ids, auto_reset=False, action_format="codes")
+        r_h = float(r.cpu()[0])
+        done = bool(d.cpu()[0])
+        snap = _snapshot(eng)
+        eng._snap = snap
+        self._refresh(snap)
+        infos = {}
+        if done:
+            infos["total_reward"] = self.total_reward
+            infos["total_time_steps"] = self.t
+        return self._state_dict(), (0 if r_h == 0.0 else r_h), done, infos
+
+    def check_terminate(self):
+        if self.t == self.max_time_steps:
+            return True
+        return all(p.status == "delivered" for p in self.packages)
+
+    def is_free_cell(self, position):
+        r, c = position
+        if r < 0 or r >= self.n_rows or c < 0 or c >= self.n_cols:
+            return False
+        return self.grid[r][c] == 0
+
+    def valid_position(self, pos):
+        r, c = pos
+        if r < 0 or r >= self.n_rows or c < 0 or c >= self.n_cols:
+            return False
+        return self.grid[r][c] != 1
+
+    def compute_new_position(self, position, move):
+        r, c = position
+        return {"S": (r, c), "L": (r, c - 1), "R": (r, c + 1), "U": (r - 1, c), "D": (r + 1, c)}.get(move, (r, c))
+
+    def render(self):
+        grid_copy = [row[:] for row in self.grid]
+        for i, robot in enumerate(self.robots):
+            r, c = robot.position
+            grid_copy[r][c] = "R%i" % i
+        for row in grid_copy:
+            print("\t".join(str(cell) for cell in row))
+
+    def render_pygame(self, cell_size=40):  # headless engine
+        return None
+
+
+def _snapshot(engine: BatchedEnv):
+    s = engine.read_state()
+    return {k: v.cpu().numpy() for k, v in s.items() if k in ("robots", "pkgs", "t", "total_reward")}
+
+
+class VectorizedEnv:
+    """MAPPO/env_vectorized.py:1-24 + QMIX ``indices=`` (QMIX/env_vectorized.py:13-37).
+
+    One BatchedEnv holds all envs; env i is seeded ``seed + i``.
+    """
+
+    def __init__(self, env_cls=None, num_envs=1, **env_kwargs):
+        map_file = env_kwargs.get("map_file")
+        grid = load_map(map_path(map_file))
+        base_seed = env_kwargs.get("seed", None)
+        # MAPPO/env_vectorized.py:4-10: seed + idx, or the Environment default
+        seeds = [base_seed + i for i in range(num_envs)] if base_seed is not None else [2025] * num_envs
+        n_robots = env_kwargs.get("n_robots", 5)
+        n_packages = env_kwargs.get("n_packages", 20)
+        T = env_kwargs.get("max_time_steps", 100)
+        self.engine = BatchedEnv(grid_array(grid), num_envs, n_robots, n_packages, T,
+                                 env_kwargs.get("move_cost", -0.01), env_kwargs.get("delivery_reward", 10.),
+                                 env_kwargs.get("delay_reward", 1.), seeds=seeds, tracker="fresh")
+        self.engine._grid_list = grid
+        self.engine._snap = None
+        self.envs = [Environment(map_file, T, n_robots, n_packages, env_kwargs.get("move_cost", -0.01),
+                                 env_kwargs.get("delivery_reward", 10.), env_kwargs.get("delay_reward", 1.),
+                                 seeds[i], _engine=self.engine, _idx=i) for i in range(num_envs)]
+        self.num_envs = num_envs
+
+    def _refresh_all(self):
+        snap = _snapshot(self.engine)
+        self.engine._snap = snap
+        for env in self.envs:
+            env._refresh(snap)
+
+    def reset(self, indices=None):
+        idx = list(range(self.num_envs)) if indices is None else list(indices)
+        self.engine.reset(None if indices is None else idx)
+        self._refresh_all()
+        return [self.envs[i]._state_dict() for i in idx]
+
+    def step(self, actions, indices=None):
+        idx = list(range(self.num_envs)) if indices is None else list(indices)
+        if len(actions) != len(idx):
+            raise ValueError("one action list per stepped env")
+        codes = np.stack([encode_actions(a, self.envs[i].n_robots) for i, a in zip(idx, actions)])
+        eng = self.engine
+        a = torch.from_numpy(codes).to(eng.device)
+        r, _, d = eng.step(a, env_ids=None if indices is None else idx, auto_reset=False, action_format="codes")
+        r_h = r.cpu().numpy()
+        d_h = d.cpu().numpy().astype(bool)
+        self._refresh_all()
+        states, rewards, dones, infos = [], [], [], []
+        for k, i in enumerate(idx):
+            env = self.envs[i]
+            states.append(env._state_dict())
+            rewards.append(0 if r_h[k] == 0.0 else float(r_h[k]))
+            dones.append(bool(d_h[k]))
+            info = {}
+            if d_h[k]:
+                info = {"total_reward": env.total_reward, "total_time_steps": env.t}
+            infos.append(info)
+        return states, rewards, dones, infos
+
+    def render(self, indices=None):
+        return None

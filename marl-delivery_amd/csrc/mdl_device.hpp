@@ -37,6 +37,18 @@ struct MapDesc {
     int pad;
 };
 
+// Per-env scalars, one 16-byte record (one load / one store per step).
+struct __align__(16) EnvScalars {
+    int32_t t;       // Environment.t
+    uint32_t ctr;    // tracker insertion counter (stale mode)
+    double total;    // Environment.total_reward (fp64, as the reference's Python float)
+};
+
+// Per-package state byte: bits 0-1 env status (ST_*), then the persistent
+// tracker's view of the same id (stale mode): present, in_transit, survivor
+// (inserted in an earlier episode -> its data lives in `trk`, not `pkg`).
+enum : uint32_t { PS_STATUS = 3u, PS_PRESENT = 4u, PS_TRANSIT = 8u, PS_SURVIVOR = 16u };
+
 // Everything a kernel needs about the engine, passed by value.
 struct DevParams {
     int E, A, P, T;
@@ -47,24 +59,20 @@ struct DevParams {
     int n_maps;
     MapDesc maps[MAX_MAPS];
     const uint8_t* grids;
+    const uint8_t* movevalid;  // per map cell: bit m set if move code m (L,R,U,D = 1..4) stays on a free cell
     const uint16_t* free_cells;
     const uint16_t* rank;
-    const uint8_t* env_map;   // [E] or null
+    const uint8_t* env_map;    // [E] or null
     // state (SoA, env-major)
-    uint16_t* rob;            // [E][A] r | c<<8
-    uint16_t* carry;          // [E][A]
-    uint64_t* pkg;            // [E][P] sr|sc<<8|tr<<16|tc<<24|st<<32|dl<<48
-    uint8_t* status;          // [E][P]
-    int32_t* t;               // [E]
-    double* total;            // [E]
-    uint32_t* mt;             // [E][624]
-    int32_t* mt_pos;          // [E]
-    uint8_t* trk_flag;        // [E][P] bit0 present, bit1 in_transit  (stale mode)
-    uint32_t* trk_seq;        // [E][P] insertion order                 (stale mode)
-    uint64_t* trk_pkg;        // [E][P] data copy at insertion          (stale mode)
-    uint32_t* trk_ctr;        // [E]
-    double* ep_total;         // [E] total_reward of the last finished episode
-    int32_t* ep_len;          // [E]
+    uint32_t* rob;             // [E][A] cell (r | c<<8) | carrying << 16
+    uint64_t* pkg;             // [E][P] sr|sc<<8|tr<<16|tc<<24|st<<32|dl<<48 (cells packed r|c<<8)
+    uint8_t* pstate;           // [E][P] PS_* bits
+    EnvScalars* es;            // [E]
+    uint32_t* mt;              // [E][624]
+    int32_t* mt_pos;           // [E]
+    uint4* trk;                // [E][P] stale mode: (data lo, data hi, insertion seq, 0)
+    double* ep_total;          // [E] total_reward of the last finished episode
+    int32_t* ep_len;           // [E]
 };
 
 // ---------------------------------------------------------------- wave utils
@@ -273,28 +281,31 @@ __device__ inline int reset_env(MTState& mt, const DevParams& p, const MapDesc& 
 // deadline / id / iteration order.
 struct TrkFresh {  // == env truth: ids in spawn (= id) order
     const uint64_t* pk;
-    const uint8_t* st;
+    const uint8_t* ps;
     int n;
     __device__ int count() const { return n; }
-    __device__ bool present(int j) const { const int s = st[j]; return s == ST_WAITING || s == ST_IN_TRANSIT; }
-    __device__ bool in_transit(int j) const { return st[j] == ST_IN_TRANSIT; }
+    __device__ bool present(int j) const { const int s = ps[j] & PS_STATUS; return s == ST_WAITING || s == ST_IN_TRANSIT; }
+    __device__ bool in_transit(int j) const { return (ps[j] & PS_STATUS) == ST_IN_TRANSIT; }
     __device__ uint64_t data(int j) const { return pk[j]; }
     __device__ int id(int j) const { return j + 1; }
     __device__ uint32_t order(int j) const { return (uint32_t)j; }
     __device__ int slot_of(int id) const { return (id >= 1 && id <= n && present(id - 1)) ? id - 1 : -1; }
 };
 
-struct TrkStale {  // explicit per-id slots (never cleared on auto-reset)
-    const uint8_t* flag;
-    const uint32_t* seq;
-    const uint64_t* pk;
+// Explicit per-id slots, never cleared on auto-reset.  Iteration order:
+// survivors of earlier episodes by insertion seq, then this episode's
+// insertions, which happen in id order (spawn order == id order).
+struct TrkStale {
+    const uint8_t* ps;
+    const uint64_t* td;   // survivor ? trk data : pkg
+    const uint32_t* tq;   // survivor ? seq : 0x80000000 + id
     int n;
     __device__ int count() const { return n; }
-    __device__ bool present(int j) const { return flag[j] & 1; }
-    __device__ bool in_transit(int j) const { return (flag[j] & 2) != 0; }
-    __device__ uint64_t data(int j) const { return pk[j]; }
+    __device__ bool present(int j) const { return (ps[j] & PS_PRESENT) != 0; }
+    __device__ bool in_transit(int j) const { return (ps[j] & PS_TRANSIT) != 0; }
+    __device__ uint64_t data(int j) const { return td[j]; }
     __device__ int id(int j) const { return j + 1; }
-    __device__ uint32_t order(int j) const { return seq[j]; }
+    __device__ uint32_t order(int j) const { return tq[j]; }
     __device__ int slot_of(int id) const { return (id >= 1 && id <= n && present(id - 1)) ? id - 1 : -1; }
 };
 

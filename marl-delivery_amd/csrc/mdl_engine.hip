@@ -150,7 +150,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     }
 
     // ---- maps ----
-    std::vector<uint8_t> allgrid;
+    std::vector<uint8_t> allgrid, allvalid;
     std::vector<uint16_t> allfree, allrank;
     mdl::DevParams& p = eng->p;
     size_t goff = 0;
@@ -175,6 +175,14 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
                 return fail("map %d: cells must be 0 or 1", m);
             }
             allgrid.push_back(g[i]);
+            // valid_position (env.py:336-345) of each move, bit = move code L1 R2 U3 D4
+            const int r = i / W, col = i % W;
+            uint8_t vm = 0;
+            if (col - 1 >= 0 && g[i - 1] != 1) vm |= 1u << 1;
+            if (col + 1 < W && g[i + 1] != 1) vm |= 1u << 2;
+            if (r - 1 >= 0 && g[i - W] != 1) vm |= 1u << 3;
+            if (r + 1 < H && g[i + W] != 1) vm |= 1u << 4;
+            allvalid.push_back(vm);
             if (g[i] == 0) {
                 allfree.push_back((uint16_t)((i / W) | ((i % W) << 8)));
                 nf++;
@@ -230,27 +238,22 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     p.n_maps = n_maps;
 
     const size_t E = c.n_envs, A = c.n_robots, P = c.n_packages;
-    uint8_t* d_grid = nullptr;
+    uint8_t *d_grid = nullptr, *d_valid = nullptr;
     uint16_t *d_free = nullptr, *d_rank = nullptr;
     uint8_t* d_em = nullptr;
     int rc = 0;
     rc |= eng->alloc(&d_grid, allgrid.size());
+    rc |= eng->alloc(&d_valid, allvalid.size());
     rc |= eng->alloc(&d_free, allfree.size());
     rc |= eng->alloc(&d_rank, allrank.size());
     if (env_map) rc |= eng->alloc(&d_em, E);
     rc |= eng->alloc(&p.rob, E * A);
-    rc |= eng->alloc(&p.carry, E * A);
     rc |= eng->alloc(&p.pkg, E * P);
-    rc |= eng->alloc(&p.status, E * P);
-    rc |= eng->alloc(&p.t, E);
-    rc |= eng->alloc(&p.total, E);
+    rc |= eng->alloc(&p.pstate, E * P);
+    rc |= eng->alloc(&p.es, E);
     rc |= eng->alloc(&p.mt, E * mdl::MT_N);
     rc |= eng->alloc(&p.mt_pos, E);
-    const size_t tE = p.stale ? E : 1;
-    rc |= eng->alloc(&p.trk_flag, tE * P);
-    rc |= eng->alloc(&p.trk_seq, tE * P);
-    rc |= eng->alloc(&p.trk_pkg, tE * P);
-    rc |= eng->alloc(&p.trk_ctr, tE);
+    rc |= eng->alloc(&p.trk, (p.stale ? E : 1) * P);
     rc |= eng->alloc(&p.ep_total, E);
     rc |= eng->alloc(&p.ep_len, E);
     if (rc) {
@@ -259,6 +262,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         return fail("%s", msg.c_str());
     }
     if (hipMemcpy(d_grid, allgrid.data(), allgrid.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_valid, allvalid.data(), allvalid.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_free, allfree.data(), allfree.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_rank, allrank.data(), allrank.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         (env_map && hipMemcpy(d_em, em.data(), E, hipMemcpyHostToDevice) != hipSuccess)) {
@@ -266,6 +270,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         return fail("hipMemcpy of map tables failed");
     }
     p.grids = d_grid;
+    p.movevalid = d_valid;
     p.free_cells = d_free;
     p.rank = d_rank;
     p.env_map = d_em;

@@ -1,86 +1,49 @@
 // mdl_kernels.hip -- gfx950 kernels of the marl-delivery batched step engine.
 //
-//   k_seed       RandomState(seed) + the constructor's reset   env.py:40-41
-//   k_reset      Environment.reset()                           env.py:81-125
-//   k_step<S>    Environment.step + compute_shaped_rewards + tracker update
-//                + reset-on-done                               env.py:173-316,
-//                MAPPO/helper.py:257-369, MAPPO/trainer.py:95-130,211-257
-//   k_obs<S>     convert_observation / generate_vector_features /
-//                convert_global_state for every agent          MAPPO/helper.py:6-255
-//   k_views_*    the same builders / shaping fed from packed dict views
+//   k_seed         RandomState(seed) + the constructor's reset  env.py:40-41
+//   k_reset        Environment.reset()                          env.py:81-125
+//   k_step<S,NCH>  Environment.step + compute_shaped_rewards + tracker update
+//                  + reset-on-done                              env.py:173-316,
+//                  MAPPO/helper.py:257-369, MAPPO/trainer.py:95-130,211-257
+//   k_obs<S>       convert_observation / generate_vector_features /
+//                  convert_global_state for every agent         MAPPO/helper.py:6-255
+//   k_views_*      the same builders / shaping fed from packed dict views
+//   k_export       int32 snapshot of the SoA state
 //
 // One wavefront per env; `wpb` envs per 256-thread workgroup, each with its
 // own LDS slice of `lds_stride` bytes (dynamic shared memory).  Waves never
-// block on each other, so a workgroup's envs may take different paths
-// (e.g. one of them resetting).
+// block on each other, so a workgroup's envs may take different paths.
+//
+// k_step keeps the whole env in registers: robot a on lane a, package j on
+// lane j%64 of chunk j/64 (NCH chunks, compile-time).  Cross-lane work is
+// readlane / ballot only; LDS is touched only when an env resets.
 #include "mdl_kernels.hpp"
 #include "mdl_features.hpp"
 
 namespace mdl {
 
-// --------------------------------------------------------------- LDS carve
-struct StepLds {
-    uint64_t* pk;       // [P] package table
-    uint64_t* scratch;  // [P] reset scratch
-    uint64_t* tpk;      // [P] tracker data (stale)
+// --------------------------------------------------------------- reset LDS
+struct ResetLds {
+    uint64_t* pk;       // [P] new package table
+    uint64_t* scratch;  // [P]
     uint32_t* mt;       // [624]
-    uint32_t* tseq;     // [P]
     uint16_t* taken;    // [64]
-    uint8_t* pst;       // [P] status
-    uint8_t* pst0;      // [P] status before the step (fresh tracker_prev)
-    uint8_t* tflag;     // [P]
+    uint8_t* pst;       // [P]
 };
 
-__host__ __device__ inline size_t step_lds_bytes(int P) {
-    return align16(8 * (size_t)P) * 3 + align16(4 * MT_N) + align16(4 * (size_t)P) + align16(2 * 64) +
-           align16((size_t)P) * 3;
+__host__ __device__ inline size_t reset_lds_bytes(int P) {
+    return align16(8 * (size_t)P) * 2 + align16(4 * MT_N) + align16(2 * 64) + align16((size_t)P);
 }
 
-__device__ inline StepLds step_carve(unsigned char* b, int P) {
-    StepLds L;
+__device__ inline ResetLds reset_carve(unsigned char* b, int P) {
+    ResetLds L;
     size_t o = 0;
     L.pk = (uint64_t*)(b + o); o += align16(8 * (size_t)P);
     L.scratch = (uint64_t*)(b + o); o += align16(8 * (size_t)P);
-    L.tpk = (uint64_t*)(b + o); o += align16(8 * (size_t)P);
     L.mt = (uint32_t*)(b + o); o += align16(4 * MT_N);
-    L.tseq = (uint32_t*)(b + o); o += align16(4 * (size_t)P);
     L.taken = (uint16_t*)(b + o); o += align16(2 * 64);
-    L.pst = b + o; o += align16((size_t)P);
-    L.pst0 = b + o; o += align16((size_t)P);
-    L.tflag = b + o;
+    L.pst = b + o;
     return L;
-}
-
-// Tracker update with the current state (MAPPO/trainer.py:95-130), explicit
-// per-id slots: insert ids spawned at t (state['packages']) that are absent,
-// in id order; then carried -> in_transit, in_transit & not carried -> delete.
-__device__ inline void stale_tracker_update(StepLds& L, int P, int A, int carry, int t, uint32_t& ctr) {
-    const int lane = lane_id();
-    for (int j0 = 0; j0 < P; j0 += WAVE) {
-        const int j = j0 + lane;
-        const bool ins = j < P && pk_st(L.pk[j]) == t && !(L.tflag[j] & 1);
-        const uint64_t b = ballot(ins);
-        if (ins) {
-            L.tflag[j] = 1;
-            L.tseq[j] = ctr + (uint32_t)popc64(b & lanemask_lt());
-            L.tpk[j] = L.pk[j];
-        }
-        ctr += (uint32_t)popc64(b);
-    }
-    wave_sync();
-    for (int j0 = 0; j0 < P; j0 += WAVE) {
-        const int j = j0 + lane;
-        bool carried = false;
-        for (int i = 0; i < A; i++) carried |= rdl(carry, i) == j + 1;
-        if (j < P) {
-            const uint8_t f = L.tflag[j];
-            if (f & 1) {
-                if (carried) L.tflag[j] = 3;
-                else if (f & 2) L.tflag[j] = 0;
-            }
-        }
-    }
-    wave_sync();
 }
 
 __device__ inline void load_mt(const DevParams& p, int e, uint32_t* key) {
@@ -95,41 +58,57 @@ __device__ inline void store_mt(const DevParams& p, int e, const uint32_t* key, 
     if (lane_id() == 0) p.mt_pos[e] = pos;
 }
 
-// Write robots / packages / statuses / clock after a reset (or seed).
-__device__ inline void store_layout(const DevParams& p, int e, const StepLds& L, int cell) {
+// One Environment.reset() (env.py:81-125) into LDS; returns this lane's robot cell.
+__device__ inline int do_reset(const DevParams& p, int e, const MapDesc& md, ResetLds& L, bool seeded_in_lds) {
+    if (!seeded_in_lds) load_mt(p, e, L.mt);
+    MTState ms{L.mt, seeded_in_lds ? MT_N : p.mt_pos[e]};
+    const int cell = reset_env(ms, p, md, L.pk, L.pst, L.scratch, L.taken);
+    store_mt(p, e, L.mt, ms.pos);
+    return cell;
+}
+
+// Tracker update on lane-resident package state (MAPPO/trainer.py:95-130):
+// insert ids spawned at t that are absent (in id order), then carried ->
+// in_transit, in_transit & not carried -> delete.
+template <int NCH>
+__device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[NCH], uint32_t (&tq)[NCH],
+                                           bool (&dirty)[NCH], const uint64_t (&pk)[NCH], int P, int A, int carry,
+                                           int t, uint32_t& ctr) {
     const int lane = lane_id();
-    if (lane < p.A) {
-        p.rob[(size_t)e * p.A + lane] = (uint16_t)cell;
-        p.carry[(size_t)e * p.A + lane] = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * WAVE + lane;
+        const bool ins = j < P && pk_st(pk[c]) == t && !(ps[c] & PS_PRESENT);
+        const uint64_t b = ballot(ins);
+        if (ins) {
+            ps[c] = (ps[c] & PS_STATUS) | PS_PRESENT;
+            td[c] = pk[c];
+            tq[c] = ctr + (uint32_t)popc64(b & lanemask_lt());  // insertion seq (stored)
+            dirty[c] = true;
+        }
+        ctr += (uint32_t)popc64(b);
     }
-    for (int j = lane; j < p.P; j += WAVE) {
-        p.pkg[(size_t)e * p.P + j] = L.pk[j];
-        p.status[(size_t)e * p.P + j] = L.pst[j];
-    }
-    if (lane == 0) {
-        p.t[e] = 0;
-        p.total[e] = 0.0;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int id = c * WAVE + lane + 1;
+        bool carried = false;
+        for (int i = 0; i < A; i++) carried |= rdl(carry, i) == id;
+        if (ps[c] & PS_PRESENT) {
+            if (carried) ps[c] |= PS_TRANSIT;
+            else if (ps[c] & PS_TRANSIT) ps[c] &= PS_STATUS;
+        }
     }
 }
 
-__device__ inline void load_tracker(const DevParams& p, int e, StepLds& L) {
-    for (int j = lane_id(); j < p.P; j += WAVE) {
-        const size_t g = (size_t)e * p.P + j;
-        L.tflag[j] = p.trk_flag[g];
-        L.tseq[j] = p.trk_seq[g];
-        L.tpk[j] = p.trk_pkg[g];
+// min over lanes of v (< 1024) where valid; 1023 if none.  Ballot bisection.
+__device__ __forceinline__ int wave_min10(bool valid, int v) {
+    int m = 0;
+#pragma unroll
+    for (int b = 9; b >= 0; b--) {
+        const bool cand = valid && ((v >> b) == (m >> b));
+        if (ballot(cand) == 0) m |= 1 << b;
     }
-    wave_sync();
-}
-
-__device__ inline void store_tracker(const DevParams& p, int e, const StepLds& L, uint32_t ctr) {
-    for (int j = lane_id(); j < p.P; j += WAVE) {
-        const size_t g = (size_t)e * p.P + j;
-        p.trk_flag[g] = L.tflag[j];
-        p.trk_seq[g] = L.tseq[j];
-        p.trk_pkg[g] = L.tpk[j];
-    }
-    if (lane_id() == 0) p.trk_ctr[e] = ctr;
+    return m;
 }
 
 // ------------------------------------------------------------------ seed
@@ -137,11 +116,12 @@ __global__ __launch_bounds__(256) void k_seed(DevParams p, const uint32_t* __res
                                               int lds_stride) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int wave = threadIdx.x >> 6;
+    const int lane = lane_id();
     const int e = blockIdx.x * wpb + wave;
     if (wave >= wpb || e >= p.E) return;
-    StepLds L = step_carve(smem + (size_t)wave * lds_stride, p.P);
+    ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, p.P);
     const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
-    if (lane_id() == 0) {  // init_genrand: a serial recurrence
+    if (lane == 0) {  // init_genrand: a serial recurrence
         uint32_t s = seeds[e];
         for (int i = 0; i < MT_N; i++) {
             L.mt[i] = s;
@@ -149,45 +129,78 @@ __global__ __launch_bounds__(256) void k_seed(DevParams p, const uint32_t* __res
         }
     }
     wave_sync();
-    MTState ms{L.mt, MT_N};
-    const int cell = reset_env(ms, p, md, L.pk, L.pst, L.scratch, L.taken);
-    store_layout(p, e, L, cell);
-    store_mt(p, e, L.mt, ms.pos);
-    if (p.stale) {  // the trainer's dict starts empty (MAPPO/trainer.py:92)
-        for (int j = lane_id(); j < p.P; j += WAVE) {
-            const size_t g = (size_t)e * p.P + j;
-            p.trk_flag[g] = 0;
-            p.trk_seq[g] = 0;
-            p.trk_pkg[g] = 0;
-        }
-        if (lane_id() == 0) p.trk_ctr[e] = 0;
+    const int cell = do_reset(p, e, md, L, true);
+    if (lane < p.A) p.rob[(size_t)e * p.A + lane] = (uint32_t)cell;
+    for (int j = lane; j < p.P; j += WAVE) {
+        const size_t g = (size_t)e * p.P + j;
+        p.pkg[g] = L.pk[j];
+        p.pstate[g] = L.pst[j];  // tracker empty (MAPPO/trainer.py:92)
     }
-    if (lane_id() == 0) {
+    if (lane == 0) {
+        EnvScalars s;
+        s.t = 0;
+        s.ctr = 0;
+        s.total = 0.0;
+        p.es[e] = s;
         p.ep_total[e] = 0.0;
         p.ep_len[e] = 0;
     }
 }
 
 // ------------------------------------------------------------------ reset
+// Environment.reset() for listed envs.  Stale tracker: present entries become
+// survivors, then the update with the reset state (no clear).
+template <int NCH>
 __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restrict__ env_ids, int n, int wpb,
                                                int lds_stride) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int wave = threadIdx.x >> 6;
+    const int lane = lane_id();
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
     const int e = env_ids ? env_ids[w] : w;
-    StepLds L = step_carve(smem + (size_t)wave * lds_stride, p.P);
+    const int A = p.A, P = p.P;
+    ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
     const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
-    load_mt(p, e, L.mt);
-    MTState ms{L.mt, p.mt_pos[e]};
-    const int cell = reset_env(ms, p, md, L.pk, L.pst, L.scratch, L.taken);
-    store_layout(p, e, L, cell);
-    store_mt(p, e, L.mt, ms.pos);
-    if (p.stale) {
-        load_tracker(p, e, L);
-        uint32_t ctr = p.trk_ctr[e];
-        stale_tracker_update(L, p.P, p.A, 0, 0, ctr);
-        store_tracker(p, e, L, ctr);
+    uint32_t ps[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * WAVE + lane;
+        ps[c] = j < P ? p.pstate[(size_t)e * P + j] : 0u;
+    }
+    const int cell = do_reset(p, e, md, L, false);
+    uint32_t ctr = p.es[e].ctr;
+    uint64_t pk[NCH], td[NCH];
+    uint32_t tq[NCH];
+    bool dirty[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * WAVE + lane;
+        pk[c] = j < P ? L.pk[j] : 0;
+        const uint32_t trk = (ps[c] & PS_PRESENT) ? ((ps[c] & ~PS_STATUS) | PS_SURVIVOR) : 0u;
+        ps[c] = (j < P ? L.pst[j] : 0u) | (p.stale ? trk : 0u);
+        td[c] = pk[c];
+        tq[c] = 0;
+        dirty[c] = false;
+    }
+    if (p.stale) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, 0, 0, ctr);
+    if (lane < A) p.rob[(size_t)e * A + lane] = (uint32_t)cell;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * WAVE + lane;
+        if (j < P) {
+            const size_t g = (size_t)e * P + j;
+            p.pkg[g] = pk[c];
+            p.pstate[g] = (uint8_t)ps[c];
+            if (dirty[c]) p.trk[g] = make_uint4((uint32_t)td[c], (uint32_t)(td[c] >> 32), tq[c], 0u);
+        }
+    }
+    if (lane == 0) {
+        EnvScalars s;
+        s.t = 0;
+        s.ctr = ctr;
+        s.total = 0.0;
+        p.es[e] = s;
     }
 }
 
@@ -198,13 +211,13 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
     const int e = env_ids ? env_ids[w] : w;
     for (int j = lane_id(); j < p.P; j += WAVE) {
         const size_t g = (size_t)e * p.P + j;
-        p.trk_flag[g] = 0;
+        p.pstate[g] &= (uint8_t)PS_STATUS;
     }
-    if (lane_id() == 0) p.trk_ctr[e] = 0;
+    if (lane_id() == 0) p.es[e].ctr = 0;
 }
 
 // ------------------------------------------------------------------- step
-template <bool STALE>
+template <bool STALE, int NCH>
 __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __restrict__ actions, int fmt,
                                               const int* __restrict__ env_ids, int n, int auto_reset,
                                               double* __restrict__ r_out, float* __restrict__ sh_out,
@@ -216,101 +229,129 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     if (wave >= wpb || w >= n) return;
     const int e = env_ids ? env_ids[w] : w;
     const int A = p.A, P = p.P;
-    StepLds L = step_carve(smem + (size_t)wave * lds_stride, P);
-    const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
-    const int H = md.H, W = md.W;
-    const uint8_t* grid = p.grids + md.grid_off;
+    const int mi = p.env_map ? p.env_map[e] : 0;
+    const MapDesc md = p.maps[mi];
 
-    // ---- load (robots on lanes, packages into LDS) ----
+    // ---- loads: one round trip, everything independent ----
+    const EnvScalars es = p.es[e];
     const bool act = lane < A;
-    const int t0 = p.t[e];
-    int cell = act ? (int)p.rob[(size_t)e * A + lane] : 0;
-    int carry = act ? (int)p.carry[(size_t)e * A + lane] : 0;
+    const uint32_t rv = act ? p.rob[(size_t)e * A + lane] : 0u;
+    const int araw = act ? (int)actions[(size_t)w * A + lane] : 0;
+    uint64_t pk[NCH], td[NCH];
+    uint32_t ps[NCH], ps0[NCH], tq[NCH];
+    bool dirty[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * WAVE + lane;
+        pk[c] = 0;
+        ps[c] = 0;
+        td[c] = 0;
+        tq[c] = 0;
+        dirty[c] = false;
+        if (j < P) {
+            const size_t g = (size_t)e * P + j;
+            pk[c] = p.pkg[g];
+            ps[c] = p.pstate[g];
+            if (STALE) {
+                const uint4 v = p.trk[g];
+                td[c] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                tq[c] = v.z;
+            }
+        }
+        ps0[c] = ps[c];
+    }
     int mv = MV_S, op = 0;
-    if (act) decode_action(actions[(size_t)w * A + lane], fmt, mv, op);
-    for (int j = lane; j < P; j += WAVE) {
-        const size_t g = (size_t)e * P + j;
-        L.pk[j] = p.pkg[g];
-        const uint8_t s = p.status[g];
-        L.pst[j] = s;
-        L.pst0[j] = s;
-        if (STALE) {
-            L.tflag[j] = p.trk_flag[g];
-            L.tseq[j] = p.trk_seq[g];
-            L.tpk[j] = p.trk_pkg[g];
+    if (act) decode_action(araw, fmt, mv, op);
+    int cell = (int)(rv & 0xffffu), carry = (int)(rv >> 16);
+    const int t0 = es.t;
+    // tracker_prev view: data / iteration order per slot
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int id = c * WAVE + lane + 1;
+        if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
+            td[c] = pk[c];
+            tq[c] = STALE ? 0x80000000u + (uint32_t)id : (uint32_t)id;
         }
     }
-    wave_sync();
 
     // ---- movement (env.py:188-257) ----
     // moved = least fixed point of
     //   moved[i] = mover[i] & winner(prop[i]) == i & (occ(prop[i]) none | moved[occ])
-    // winner = lowest-index mover into the cell; equivalent to the reference's
-    // restart-from-zero loop (checked against the oracle's literal
-    // restatement of that loop).
-    const int prev_cell = cell, prev_carry = carry;
+    // winner = lowest-index mover into the cell: the reference's restart-from-0
+    // loop, checked against the oracle's literal restatement.
+    const int pcell = cell, pcarry = carry;
     int prop = cell;
-    {
-        int nr = cell_r(cell), nc = cell_c(cell);
-        if (mv == MV_L) nc -= 1;
-        else if (mv == MV_R) nc += 1;
-        else if (mv == MV_U) nr -= 1;
-        else if (mv == MV_D) nr += 1;
-        if (nr >= 0 && nr < H && nc >= 0 && nc < W && grid[nr * W + nc] != 1) prop = nr | (nc << 8);
+    if (act && mv >= MV_L && mv <= MV_D) {
+        const int ci = cell_r(cell) * md.W + cell_c(cell);
+        const uint32_t vm = p.movevalid[md.grid_off + ci];
+        if ((vm >> mv) & 1u) prop = cell + (mv == MV_L ? -256 : mv == MV_R ? 256 : mv == MV_U ? -1 : 1);
     }
     const bool mover = act && prop != cell;
     const uint64_t movers = ballot(mover);
-    bool win = true;
-    int occ = -1;
-    for (int j = 0; j < A; j++) {
-        const int pj = rdl(cell, j), qj = rdl(prop, j);
-        if (j < lane && ((movers >> j) & 1) && qj == prop) win = false;
-        if (pj == prop) occ = j;
-    }
     uint64_t moved = 0;
-    for (int it = 0; it <= A; it++) {
-        const bool m = mover && win && (occ < 0 || ((moved >> occ) & 1ull));
-        const uint64_t nm = ballot(m);
-        if (nm == moved) break;
-        moved = nm;
+    if (movers) {
+        bool win = true;
+        int occ = -1;
+        for (int j = 0; j < A; j++) {
+            const int pj = rdl(cell, j), qj = rdl(prop, j);
+            if (j < lane && ((movers >> j) & 1ull) && qj == prop) win = false;
+            if (pj == prop) occ = j;
+        }
+        const bool base = mover && win;
+        for (int it = 0; it <= A; it++) {
+            const bool m = base && (occ < 0 || ((moved >> occ) & 1ull));
+            const uint64_t nm = ballot(m);
+            if (nm == moved) break;
+            moved = nm;
+        }
+        if ((moved >> lane) & 1ull) cell = prop;
     }
-    if ((moved >> lane) & 1ull) cell = prop;
     const int n_cost = popc64(moved);
 
-    // ---- package actions (env.py:259-292) ----
+    // ---- package actions (env.py:259-292); robots sit on distinct cells, so
+    // pick-ups and drops of different robots never interact ----
     uint64_t pickers = ballot(act && op == 1 && carry == 0);
     while (pickers) {
         const int i = ffs64(pickers);
         pickers &= pickers - 1;
         const int ci = rdl(cell, i);
         int found = -1;
-        for (int j0 = 0; j0 < P; j0 += WAVE) {
-            const int j = j0 + lane;
-            const bool cand = j < P && L.pst[j] == ST_WAITING && pk_start(L.pk[j]) == ci;
-            const uint64_t b = ballot(cand);
-            if (b) {
-                found = j0 + ffs64(b);
-                break;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            if (found < 0) {
+                const uint64_t b = ballot((ps[c] & PS_STATUS) == ST_WAITING && pk_start(pk[c]) == ci);
+                if (b) {
+                    const int jj = ffs64(b);
+                    found = c * WAVE + jj;
+                    if (lane == jj) ps[c] = (ps[c] & ~PS_STATUS) | ST_IN_TRANSIT;
+                }
             }
         }
-        if (found >= 0) {
-            if (lane == i) carry = found + 1;
-            if (lane == 0) L.pst[found] = ST_IN_TRANSIT;
+        if (found >= 0 && lane == i) carry = found + 1;
+    }
+    uint64_t droppers = ballot(act && op == 2 && carry != 0);
+    uint64_t dmask = 0, omask = 0;
+    while (droppers) {
+        const int i = ffs64(droppers);
+        droppers &= droppers - 1;
+        const int j = rdl(carry, i) - 1;
+        const int ci = rdl(cell, i);
+        const int cc = j >> 6, jj = j & 63;
+        uint64_t v = 0;
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+            if (c == cc) v = pk[c];
+        const uint64_t d = (uint64_t)(uint32_t)rdl((int)(uint32_t)v, jj) |
+                           ((uint64_t)(uint32_t)rdl((int)(uint32_t)(v >> 32), jj) << 32);
+        if (pk_target(d) == ci) {
+            dmask |= 1ull << i;
+            if (t0 <= pk_dl(d)) omask |= 1ull << i;
+#pragma unroll
+            for (int c = 0; c < NCH; c++)
+                if (c == cc && lane == jj) ps[c] = (ps[c] & ~PS_STATUS) | ST_DELIVERED;
+            if (lane == i) carry = 0;
         }
     }
-    wave_sync();
-    bool at_tgt = false, ontime = false;
-    if (act && op == 2 && carry != 0) {
-        const uint64_t d = L.pk[carry - 1];
-        if (pk_target(d) == cell) {
-            at_tgt = true;
-            ontime = t0 <= pk_dl(d);
-            L.pst[carry - 1] = ST_DELIVERED;
-            carry = 0;
-        }
-    }
-    const uint64_t dmask = ballot(at_tgt), omask = ballot(ontime);
-    wave_sync();
     // reward: fp64 fold in the reference's order (move costs, then deliveries)
     double rr = 0.0;
     for (int k = 0; k < n_cost; k++) rr += p.move_cost;
@@ -319,79 +360,166 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         rr += ((omask >> i) & 1ull) ? p.delivery_reward : p.delay_reward;
     }
     const int t1 = t0 + 1;
-    const double total = p.total[e] + rr;
+    const double total = es.total + rr;
 
     // ---- terminate (env.py:308-316) + spawn (get_state env.py:133-137) ----
     int ndel = 0;
-    for (int j0 = 0; j0 < P; j0 += WAVE) {
-        const int j = j0 + lane;
-        bool dv = false;
-        if (j < P) {
-            dv = L.pst[j] == ST_DELIVERED;
-            if (pk_st(L.pk[j]) == t1) L.pst[j] = ST_WAITING;
-        }
-        ndel += popc64(ballot(dv));
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * WAVE + lane;
+        ndel += popc64(ballot((ps[c] & PS_STATUS) == ST_DELIVERED));
+        if (j < P && pk_st(pk[c]) == t1) ps[c] = (ps[c] & ~PS_STATUS) | ST_WAITING;
     }
     const bool done = (t1 == p.T) || (ndel == P);
-    wave_sync();
 
-    // ---- shaped reward with the pre-step tracker (MAPPO/trainer.py:211-218) ----
-    float s_a;
-    if (STALE) {
-        TrkStale trk{L.tflag, L.tseq, L.tpk, P};
-        s_a = shaped_agent(trk, p.shaping, act, prev_cell, prev_carry, cell, carry, mv, op, t0, t1);
-    } else {
-        TrkFresh trk{L.pk, L.pst0, P};
-        s_a = shaped_agent(trk, p.shaping, act, prev_cell, prev_carry, cell, carry, mv, op, t0, t1);
+    // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
+    float s_lane = 0.0f;
+    {
+        const float* C = p.shaping;
+        bool wprev[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const uint32_t f = ps0[c];
+            const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
+            wprev[c] = waiting && pk_st(td[c]) <= t0;
+        }
+        for (int a = 0; a < A; a++) {
+            const int pc = rdl(pcell, a), pcy = rdl(pcarry, a);
+            const int cc = rdl(cell, a), ccy = rdl(carry, a);
+            const int mva = rdl(mv, a), opa = rdl(op, a);
+            bool ppres = false;
+            uint64_t pdata = 0;
+            if (pcy != 0 && pcy <= P) {
+                const int j = pcy - 1, c2 = j >> 6, jj = j & 63;
+                uint32_t f = 0;
+                uint64_t d = 0;
+#pragma unroll
+                for (int c = 0; c < NCH; c++)
+                    if (c == c2) {
+                        f = ps0[c];
+                        d = td[c];
+                    }
+                f = (uint32_t)rdl((int)f, jj);
+                d = (uint64_t)(uint32_t)rdl((int)(uint32_t)d, jj) |
+                    ((uint64_t)(uint32_t)rdl((int)(uint32_t)(d >> 32), jj) << 32);
+                ppres = STALE ? (f & PS_PRESENT) != 0
+                              : ((f & PS_STATUS) == ST_WAITING || (f & PS_STATUS) == ST_IN_TRANSIT);
+                pdata = d;
+            }
+            float s = 0.0f;
+            // 1. pickup / delivery
+            if (pcy == 0 && ccy != 0) s = s + C[SH_PICK];
+            else if (pcy != 0 && ccy == 0 && ppres && cc == pk_target(pdata))
+                s = s + ((t1 <= pk_dl(pdata)) ? C[SH_ONTIME] : C[SH_LATE]);
+            const bool moved_a = pc != cc;
+            const bool need_can = opa == 1 && pcy == 0 && ccy == 0;
+            const bool need_idle = !moved_a && mva == MV_S && pcy == 0;
+            const bool need_near = moved_a && !(pcy != 0 && ppres);
+            bool can = false, idle = false;
+            int near_cell = -1;
+            if (need_can || need_idle || need_near) {
+                int dmin = 1023;
+                int dist[NCH];
+#pragma unroll
+                for (int c = 0; c < NCH; c++) {
+                    const int sc = pk_start(td[c]);
+                    dist[c] = manhattan(pc, sc);
+                    if (need_can) can |= ballot(wprev[c] && sc == cc) != 0;
+                    if (need_idle) idle |= ballot(wprev[c] && dist[c] <= 3) != 0;
+                    if (need_near) {
+                        const int m = wave_min10(wprev[c], dist[c]);
+                        dmin = m < dmin ? m : dmin;
+                    }
+                }
+                if (need_near && dmin < 1023) {
+                    // first minimum in tracker iteration order (min() over the dict)
+                    uint32_t best_o = 0xffffffffu;
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        uint64_t tie = ballot(wprev[c] && dist[c] == dmin);
+                        while (tie) {
+                            const int jj = ffs64(tie);
+                            tie &= tie - 1;
+                            const uint32_t o = (uint32_t)rdl((int)tq[c], jj);
+                            if (o < best_o) {
+                                best_o = o;
+                                near_cell = rdl(pk_start(td[c]), jj);
+                            }
+                            if (!STALE) break;  // fresh: order == id, the first tie wins
+                        }
+                        if (!STALE && best_o != 0xffffffffu) break;
+                    }
+                }
+            }
+            // 2. wasted operations
+            if (opa == 1) {
+                if (pcy != 0) s = s + C[SH_WPICK];
+                else if (ccy == 0 && !can) s = s + C[SH_WPICK];
+            } else if (opa == 2) {
+                if (pcy == 0) s = s + C[SH_WDROP];
+                else if (ccy != 0 && ppres && cc != pk_target(pdata)) s = s + C[SH_WDROP];
+            }
+            // 3. movement
+            if (mva != MV_S && !moved_a) s = s + C[SH_STUCK];
+            const int tgt = (pcy != 0 && ppres) ? pk_target(pdata) : near_cell;
+            if (tgt >= 0 && moved_a) {
+                const int db = manhattan(pc, tgt), da = manhattan(cc, tgt);
+                if (da < db) s = s + C[SH_CLOSER];
+                else if (da > db) s = s + C[SH_AWAY];
+            }
+            // 4. idle next to an available package
+            if (!moved_a && mva == MV_S && pcy == 0 && idle) s = s + C[SH_IDLE];
+            if (lane == a) s_lane = s;
+        }
     }
-    const float shaped = (float)rr + np_sum_lanes(s_a, A);
+    const float shaped = (float)rr + np_sum_lanes(s_lane, A);
 
-    // ---- tracker update with the new state; a done env that is reset here
-    // skips it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
-    uint32_t ctr = 0;
-    if (STALE) {
-        ctr = p.trk_ctr[e];
-        if (!(done && auto_reset)) stale_tracker_update(L, P, A, carry, t1, ctr);
-    }
+    // ---- tracker update with the new state; a done env that resets here skips
+    // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
+    uint32_t ctr = es.ctr;
+    const bool do_rst = done && auto_reset;
+    if (STALE && !do_rst) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, carry, t1, ctr);
 
     // ---- reset on done (MAPPO/trainer.py:230-235) ----
     int t_out = t1;
     double total_out = total;
-    bool did_reset = false;
-    if (done && auto_reset) {
-        load_mt(p, e, L.mt);
-        MTState ms{L.mt, p.mt_pos[e]};
-        const int nc = reset_env(ms, p, md, L.pk, L.pst, L.scratch, L.taken);
-        store_mt(p, e, L.mt, ms.pos);
+    if (do_rst) {
+        ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
+        const int nc = do_reset(p, e, md, L, false);
         if (act) {
             cell = nc;
             carry = 0;
         }
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const int j = c * WAVE + lane;
+            pk[c] = j < P ? L.pk[j] : 0;
+            const uint32_t trk = (ps[c] & PS_PRESENT) ? ((ps[c] & ~PS_STATUS) | PS_SURVIVOR) : 0u;
+            ps[c] = (j < P ? L.pst[j] : 0u) | (STALE ? trk : 0u);
+        }
+        if (STALE) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, 0, 0, ctr);
         t_out = 0;
         total_out = 0.0;
-        did_reset = true;
-        if (STALE) stale_tracker_update(L, P, A, 0, 0, ctr);  // tracker NOT cleared (trainer.py:233)
     }
 
-    // ---- write back ----
-    if (act) {
-        p.rob[(size_t)e * A + lane] = (uint16_t)cell;
-        p.carry[(size_t)e * A + lane] = (uint16_t)carry;
-    }
-    for (int j = lane; j < P; j += WAVE) {
-        const size_t g = (size_t)e * P + j;
-        p.status[g] = L.pst[j];
-        if (did_reset) p.pkg[g] = L.pk[j];
-        if (STALE) {
-            p.trk_flag[g] = L.tflag[j];
-            p.trk_seq[g] = L.tseq[j];
-            p.trk_pkg[g] = L.tpk[j];
+    // ---- write back only what changed ----
+    if (act) p.rob[(size_t)e * A + lane] = (uint32_t)cell | ((uint32_t)carry << 16);
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * WAVE + lane;
+        if (j < P) {
+            const size_t g = (size_t)e * P + j;
+            if (ps[c] != ps0[c]) p.pstate[g] = (uint8_t)ps[c];
+            if (do_rst) p.pkg[g] = pk[c];
+            if (STALE && dirty[c]) p.trk[g] = make_uint4((uint32_t)td[c], (uint32_t)(td[c] >> 32), tq[c], 0u);
         }
     }
     if (lane == 0) {
-        p.t[e] = t_out;
-        p.total[e] = total_out;
-        if (STALE) p.trk_ctr[e] = ctr;
+        EnvScalars s;
+        s.t = t_out;
+        s.ctr = ctr;
+        s.total = total_out;
+        p.es[e] = s;
         if (done) {
             p.ep_total[e] = total;
             p.ep_len[e] = t1;
@@ -403,16 +531,16 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
 }
 
 // ------------------------------------------------------------- observations
+// Tracker slots staged in LDS for the feature builders (random access by id).
 struct ObsLdsPre {
     uint64_t* pk;
-    uint64_t* tpk;
-    uint32_t* tseq;
-    uint8_t* pst;
-    uint8_t* tflag;
+    uint64_t* td;
+    uint32_t* tq;
+    uint8_t* ps;
 };
 
 __host__ __device__ inline size_t obs_pre_bytes(int P) {
-    return align16(8 * (size_t)P) * 2 + align16(4 * (size_t)P) + align16((size_t)P) * 2;
+    return align16(8 * (size_t)P) * 2 + align16(4 * (size_t)P) + align16((size_t)P);
 }
 
 template <bool STALE>
@@ -431,14 +559,13 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
     {
         size_t o = 0;
         S.pk = (uint64_t*)(base + o); o += align16(8 * (size_t)P);
-        S.tpk = (uint64_t*)(base + o); o += align16(8 * (size_t)P);
-        S.tseq = (uint32_t*)(base + o); o += align16(4 * (size_t)P);
-        S.pst = base + o; o += align16((size_t)P);
-        S.tflag = base + o; o += align16((size_t)P);
+        S.td = (uint64_t*)(base + o); o += align16(8 * (size_t)P);
+        S.tq = (uint32_t*)(base + o); o += align16(4 * (size_t)P);
+        S.ps = base + o;
     }
     const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
     FeatCtx c;
-    c.A = A; c.NS = P; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.t = p.t[e]; c.T = p.obsT;
+    c.A = A; c.NS = P; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.t = p.es[e].t; c.T = p.obsT;
     c.MO = p.MO; c.MP = p.MP; c.MR = p.MR; c.MPs = p.MPs;
     c.MPc = p.MP < P ? p.MP : P;
     c.MPsc = p.MPs < P ? p.MPs : P;
@@ -449,17 +576,25 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
     FeatLds L = feat_carve(base + obs_pre_bytes(P), fd);
 
     const bool act = lane < A;
-    const int cell = act ? (int)p.rob[(size_t)e * A + lane] : 0;
-    const int carry = act ? (int)p.carry[(size_t)e * A + lane] : 0;
+    const uint32_t rv = act ? p.rob[(size_t)e * A + lane] : 0u;
+    const int cell = (int)(rv & 0xffffu);
+    const int carry = (int)(rv >> 16);
     for (int j = lane; j < P; j += WAVE) {
         const size_t g = (size_t)e * P + j;
+        const uint64_t d = p.pkg[g];
+        const uint32_t f = p.pstate[g];
+        S.pk[j] = d;
+        S.ps[j] = (uint8_t)f;
         if (STALE) {
-            S.tflag[j] = p.trk_flag[g];
-            S.tseq[j] = p.trk_seq[g];
-            S.tpk[j] = p.trk_pkg[g];
-        } else {
-            S.pk[j] = p.pkg[g];
-            S.pst[j] = p.status[g];
+            uint64_t td = d;
+            uint32_t tq = 0x80000000u + (uint32_t)(j + 1);
+            if (f & PS_SURVIVOR) {
+                const uint4 v = p.trk[g];
+                td = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                tq = v.z;
+            }
+            S.td[j] = td;
+            S.tq[j] = tq;
         }
     }
     wave_sync();
@@ -479,10 +614,10 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
         }
     };
     if (STALE) {
-        TrkStale trk{S.tflag, S.tseq, S.tpk, P};
+        TrkStale trk{S.ps, S.td, S.tq, P};
         run(trk);
     } else {
-        TrkFresh trk{S.pk, S.pst, P};
+        TrkFresh trk{S.pk, S.ps, P};
         run(trk);
     }
 }
@@ -498,6 +633,16 @@ struct ViewLdsPre {
 __host__ __device__ inline size_t view_pre_bytes(int NS) {
     const int n = NS > 0 ? NS : 1;
     return align16(4 * (size_t)n) + align16(8 * (size_t)n) + align16((size_t)n);
+}
+
+__device__ inline ViewLdsPre view_carve(unsigned char* base, int NSmax) {
+    ViewLdsPre V;
+    const int nsm = NSmax > 0 ? NSmax : 1;
+    size_t o = 0;
+    V.ids = (int32_t*)(base + o); o += align16(4 * (size_t)nsm);
+    V.pk = (uint64_t*)(base + o); o += align16(8 * (size_t)nsm);
+    V.flag = base + o;
+    return V;
 }
 
 __device__ inline TrkView load_view(const int32_t* rec, ViewLdsPre& V, int& t, int& A, int& map, int& cell,
@@ -537,14 +682,7 @@ __global__ __launch_bounds__(256) void k_views_features(DevParams p, const int32
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
     unsigned char* base = smem + (size_t)wave * lds_stride;
-    ViewLdsPre V;
-    {
-        const int nsm = NSmax > 0 ? NSmax : 1;
-        size_t o = 0;
-        V.ids = (int32_t*)(base + o); o += align16(4 * (size_t)nsm);
-        V.pk = (uint64_t*)(base + o); o += align16(8 * (size_t)nsm);
-        V.flag = base + o;
-    }
+    ViewLdsPre V = view_carve(base, NSmax);
     int t, A, map, cell, carry;
     const TrkView trk = load_view(views + offs[w], V, t, A, map, cell, carry);
     const MapDesc md = p.maps[map];
@@ -582,15 +720,7 @@ __global__ __launch_bounds__(256) void k_views_shaped(DevParams p, const int32_t
     const int lane = lane_id();
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
-    unsigned char* base = smem + (size_t)wave * lds_stride;
-    ViewLdsPre V;
-    {
-        const int nsm = NSmax > 0 ? NSmax : 1;
-        size_t o = 0;
-        V.ids = (int32_t*)(base + o); o += align16(4 * (size_t)nsm);
-        V.pk = (uint64_t*)(base + o); o += align16(8 * (size_t)nsm);
-        V.flag = base + o;
-    }
+    ViewLdsPre V = view_carve(smem + (size_t)wave * lds_stride, NSmax);
     int t_prev, A, map, pcell, pcarry;
     const TrkView trk = load_view(prev + prev_offs[w], V, t_prev, A, map, pcell, pcarry);
     const int32_t* cr = cur + cur_offs[w];
@@ -618,33 +748,44 @@ __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict
     if (e >= p.E) return;
     const int A = p.A, P = p.P;
     if (robots && lane < A) {
-        const int c = p.rob[(size_t)e * A + lane];
+        const uint32_t rv = p.rob[(size_t)e * A + lane];
         int32_t* o = robots + ((size_t)e * A + lane) * 3;
-        o[0] = cell_r(c);
-        o[1] = cell_c(c);
-        o[2] = p.carry[(size_t)e * A + lane];
+        o[0] = cell_r((int)(rv & 0xffffu));
+        o[1] = cell_c((int)(rv & 0xffffu));
+        o[2] = (int)(rv >> 16);
     }
     for (int j = lane; j < P; j += WAVE) {
         const size_t g = (size_t)e * P + j;
         const uint64_t d = p.pkg[g];
-        const int st = p.status[g];
+        const uint32_t f = p.pstate[g];
+        const int st = (int)(f & PS_STATUS);
         if (pkgs) {
             int32_t* o = pkgs + g * 8;
             o[0] = cell_r(pk_start(d)); o[1] = cell_c(pk_start(d));
             o[2] = cell_r(pk_target(d)); o[3] = cell_c(pk_target(d));
             o[4] = pk_st(d); o[5] = pk_dl(d); o[6] = j + 1; o[7] = st;
         }
-        int present, intr, order;
-        uint64_t td;
+        int present, intr;
+        uint32_t order;
+        uint64_t td = d;
         if (p.stale) {
-            const int f = p.trk_flag[g];
-            present = f & 1; intr = (f >> 1) & 1; order = (int)p.trk_seq[g]; td = p.trk_pkg[g];
+            present = (f & PS_PRESENT) ? 1 : 0;
+            intr = (f & PS_TRANSIT) ? 1 : 0;
+            order = 0x80000000u + (uint32_t)(j + 1);
+            if (f & PS_SURVIVOR) {
+                const uint4 v = p.trk[g];
+                td = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                order = v.z;
+            }
         } else {
-            present = st == ST_WAITING || st == ST_IN_TRANSIT; intr = st == ST_IN_TRANSIT; order = j; td = d;
+            present = st == ST_WAITING || st == ST_IN_TRANSIT;
+            intr = st == ST_IN_TRANSIT;
+            order = (uint32_t)j;
         }
         if (trk) {
             int32_t* o = trk + g * 4;
-            o[0] = present; o[1] = intr; o[2] = order; o[3] = 0;
+            // order as a signed int32 that sorts like the unsigned key
+            o[0] = present; o[1] = intr; o[2] = (int32_t)(order ^ 0x80000000u); o[3] = (f & PS_SURVIVOR) ? 1 : 0;
         }
         if (trk_data) {
             int32_t* o = trk_data + g * 6;
@@ -654,21 +795,38 @@ __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict
         }
     }
     if (lane == 0) {
-        if (tt) tt[e] = p.t[e];
-        if (total) total[e] = p.total[e];
+        const EnvScalars s = p.es[e];
+        if (tt) tt[e] = s.t;
+        if (total) total[e] = s.total;
     }
 }
 
 // ---------------------------------------------------------------- launchers
 static int blocks_for(int n, int wpb) { return (n + wpb - 1) / wpb; }
 
+static int nch_for(int P) {
+    const int c = (P + WAVE - 1) / WAVE;
+    return c <= 1 ? 1 : c <= 2 ? 2 : c <= 4 ? 4 : c <= 8 ? 8 : 16;
+}
+
 hipError_t launch_seed(const DevParams& p, const uint32_t* seeds, int wpb, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL(k_seed, dim3(blocks_for(p.E, wpb)), dim3(256), lds * wpb, s, p, seeds, wpb, (int)lds);
     return hipGetLastError();
 }
 
+template <int NCH>
+static void launch_reset_t(const DevParams& p, const int* ids, int n, int wpb, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL(k_reset<NCH>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, ids, n, wpb, (int)lds);
+}
+
 hipError_t launch_reset(const DevParams& p, const int* ids, int n, int wpb, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL(k_reset, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, ids, n, wpb, (int)lds);
+    switch (nch_for(p.P)) {
+        case 1: launch_reset_t<1>(p, ids, n, wpb, lds, s); break;
+        case 2: launch_reset_t<2>(p, ids, n, wpb, lds, s); break;
+        case 4: launch_reset_t<4>(p, ids, n, wpb, lds, s); break;
+        case 8: launch_reset_t<8>(p, ids, n, wpb, lds, s); break;
+        default: launch_reset_t<16>(p, ids, n, wpb, lds, s); break;
+    }
     return hipGetLastError();
 }
 
@@ -677,14 +835,29 @@ hipError_t launch_tracker_clear(const DevParams& p, const int* ids, int n, hipSt
     return hipGetLastError();
 }
 
+template <bool ST, int NCH>
+static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
+                          double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((k_step<ST, NCH>), dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, actions, fmt, ids, n,
+                       auto_reset, r, sh, done, wpb, (int)lds);
+}
+
+template <bool ST>
+static void launch_step_s(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
+                          double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
+    switch (nch_for(p.P)) {
+        case 1: launch_step_t<ST, 1>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
+        case 2: launch_step_t<ST, 2>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
+        case 4: launch_step_t<ST, 4>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
+        case 8: launch_step_t<ST, 8>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
+        default: launch_step_t<ST, 16>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
+    }
+}
+
 hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
                        double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
-    if (p.stale)
-        hipLaunchKernelGGL(k_step<true>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, actions, fmt, ids, n,
-                           auto_reset, r, sh, done, wpb, (int)lds);
-    else
-        hipLaunchKernelGGL(k_step<false>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, actions, fmt, ids,
-                           n, auto_reset, r, sh, done, wpb, (int)lds);
+    if (p.stale) launch_step_s<true>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s);
+    else launch_step_s<false>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s);
     return hipGetLastError();
 }
 
@@ -724,7 +897,7 @@ hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int
     return hipGetLastError();
 }
 
-size_t step_lds(int P) { return step_lds_bytes(P); }
+size_t step_lds(int P) { return reset_lds_bytes(P); }
 size_t obs_lds(int A, int P, int HW, int MP, int MPs) {
     FeatDims d{A, P, HW, MP < P ? MP : P, MPs < P ? MPs : P};
     return obs_pre_bytes(P) + feat_lds_bytes(d);

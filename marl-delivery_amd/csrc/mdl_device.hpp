@@ -34,7 +34,7 @@ struct MapDesc {
     int free_off;   // into free_cells (u16 packed r | c<<8, row-major)
     int rank_off;   // into rank (u16) table [(2H-1)][(2W-1)]
     float inv_hw;   // 1/(H*W) for fast divmod
-    int pad;
+    int bits_off;   // into gridbits (u32 words, ceil(H*W/32) per map)
 };
 
 // Per-env scalars, one 16-byte record (one load / one store per step).
@@ -60,11 +60,12 @@ struct DevParams {
     MapDesc maps[MAX_MAPS];
     const uint8_t* grids;
     const uint8_t* movevalid;  // per map cell: bit m set if move code m (L,R,U,D = 1..4) stays on a free cell
+    const uint32_t* gridbits;  // per map obstacle bitset
     const uint16_t* free_cells;
     const uint16_t* rank;
     const uint8_t* env_map;    // [E] or null
     // state (SoA, env-major)
-    uint32_t* rob;             // [E][A] cell (r | c<<8) | carrying << 16
+    uint32_t* rob;             // [E][A] robot word, see rob_pack()
     uint64_t* pkg;             // [E][P] sr|sc<<8|tr<<16|tc<<24|st<<32|dl<<48 (cells packed r|c<<8)
     uint8_t* pstate;           // [E][P] PS_* bits
     EnvScalars* es;            // [E]
@@ -74,6 +75,16 @@ struct DevParams {
     double* ep_total;          // [E] total_reward of the last finished episode
     int32_t* ep_len;           // [E]
 };
+
+// Robot word: bits 0-15 cell (r | c<<8), bits 16-26 carried package id,
+// bits 27-30 valid_position() of the L/R/U/D neighbours of the cell (so the
+// step needs no dependent map lookup before resolving moves).
+__host__ __device__ __forceinline__ uint32_t rob_pack(int cell, int carry, uint32_t valid_mask /* bits 1..4 */) {
+    return (uint32_t)cell | ((uint32_t)carry << 16) | ((valid_mask & 0x1eu) << 26);
+}
+__host__ __device__ __forceinline__ int rob_cell(uint32_t w) { return (int)(w & 0xffffu); }
+__host__ __device__ __forceinline__ int rob_carry(uint32_t w) { return (int)((w >> 16) & 0x7ffu); }
+__host__ __device__ __forceinline__ uint32_t rob_valid(uint32_t w) { return (w >> 26) & 0x1eu; }
 
 // ---------------------------------------------------------------- wave utils
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -97,6 +108,22 @@ __device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((long long)m) 
 __device__ __forceinline__ uint64_t lanemask_lt() {
     int l = lane_id();
     return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// min over the 64 lanes (identity 0xffffffff): DPP row_shr prefix-min inside
+// each 16-lane row, then the four row results by readlane.  Wave-uniform.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    const int id = (int)0xffffffff;
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xf, 0xf, false); v = t < v ? t : v;  // row_shr:1
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xf, 0xf, false); v = t < v ? t : v;  // row_shr:2
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xf, 0xf, false); v = t < v ? t : v;  // row_shr:4
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xf, 0xf, false); v = t < v ? t : v;  // row_shr:8
+    uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, 31); m = x < m ? x : m;
+    x = (uint32_t)__builtin_amdgcn_readlane((int)v, 47); m = x < m ? x : m;
+    x = (uint32_t)__builtin_amdgcn_readlane((int)v, 63); m = x < m ? x : m;
+    return m;
 }
 
 // Correctly rounded int/int division in float32.  For |a|,|b| < 2^24 this
@@ -280,6 +307,7 @@ __device__ inline int reset_env(MTState& mt, const DevParams& p, const MapDesc& 
 // interface: slot j -> present / in_transit / start / target / start_time /
 // deadline / id / iteration order.
 struct TrkFresh {  // == env truth: ids in spawn (= id) order
+    static constexpr bool kIdIndexed = true;
     const uint64_t* pk;
     const uint8_t* ps;
     int n;
@@ -296,6 +324,7 @@ struct TrkFresh {  // == env truth: ids in spawn (= id) order
 // survivors of earlier episodes by insertion seq, then this episode's
 // insertions, which happen in id order (spawn order == id order).
 struct TrkStale {
+    static constexpr bool kIdIndexed = true;
     const uint8_t* ps;
     const uint64_t* td;   // survivor ? trk data : pkg
     const uint32_t* tq;   // survivor ? seq : 0x80000000 + id
@@ -310,6 +339,7 @@ struct TrkStale {
 };
 
 struct TrkView {  // arbitrary dict from a packed view record (dict order)
+    static constexpr bool kIdIndexed = false;
     const int32_t* ids;
     const uint8_t* flag;
     const uint64_t* pk;

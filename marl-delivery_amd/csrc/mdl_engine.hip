@@ -151,6 +151,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
 
     // ---- maps ----
     std::vector<uint8_t> allgrid, allvalid;
+    std::vector<uint32_t> allbits;
     std::vector<uint16_t> allfree, allrank;
     mdl::DevParams& p = eng->p;
     size_t goff = 0;
@@ -168,6 +169,13 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         md.free_off = (int)allfree.size();
         md.rank_off = (int)allrank.size();
         md.inv_hw = 1.0f / (float)(H * W);
+        md.bits_off = (int)allbits.size();
+        for (int w = 0; w < (H * W + 31) / 32; w++) {
+            uint32_t b = 0;
+            for (int k = 0; k < 32; k++)
+                if (w * 32 + k < H * W && grids[goff + w * 32 + k]) b |= 1u << k;
+            allbits.push_back(b);
+        }
         int nf = 0;
         for (int i = 0; i < H * W; i++) {
             if (g[i] > 1) {
@@ -210,6 +218,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         goff += (size_t)H * W;
     }
     std::vector<uint8_t> em;
+    if (env_map && n_maps == 1) env_map = nullptr;  // single map: no per-env lookup in the kernels
     if (env_map) {
         em.resize(c.n_envs);
         for (int e = 0; e < c.n_envs; e++) {
@@ -239,11 +248,13 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
 
     const size_t E = c.n_envs, A = c.n_robots, P = c.n_packages;
     uint8_t *d_grid = nullptr, *d_valid = nullptr;
+    uint32_t* d_bits = nullptr;
     uint16_t *d_free = nullptr, *d_rank = nullptr;
     uint8_t* d_em = nullptr;
     int rc = 0;
     rc |= eng->alloc(&d_grid, allgrid.size());
     rc |= eng->alloc(&d_valid, allvalid.size());
+    rc |= eng->alloc(&d_bits, allbits.size());
     rc |= eng->alloc(&d_free, allfree.size());
     rc |= eng->alloc(&d_rank, allrank.size());
     if (env_map) rc |= eng->alloc(&d_em, E);
@@ -263,6 +274,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     }
     if (hipMemcpy(d_grid, allgrid.data(), allgrid.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_valid, allvalid.data(), allvalid.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_bits, allbits.data(), allbits.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_free, allfree.data(), allfree.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_rank, allrank.data(), allrank.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         (env_map && hipMemcpy(d_em, em.data(), E, hipMemcpyHostToDevice) != hipSuccess)) {
@@ -271,13 +283,14 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     }
     p.grids = d_grid;
     p.movevalid = d_valid;
+    p.gridbits = d_bits;
     p.free_cells = d_free;
     p.rank = d_rank;
     p.env_map = d_em;
 
     eng->lds_step = mdl::step_lds((int)P);
     eng->wpb_step = waves_per_block(eng->lds_step);
-    eng->lds_obs = mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MP, p.MPs);
+    eng->lds_obs = mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MO, p.MP, p.MR, p.MPs);
     eng->wpb_obs = waves_per_block(eng->lds_obs);
     if (eng->wpb_step < 1 || eng->wpb_obs < 1) {
         delete eng;
@@ -375,7 +388,7 @@ int mdl_views_features(MdlEngine* eng, const int32_t* views, const int64_t* offs
     if (MO < 0 || MP < 0 || MR < 0 || MPs < 0) return fail("mdl_views_features: negative slot count");
     if (n_views == 0) return 0;
     const int MPc = std::min(MP, max_slots), MPsc = std::min(MPs, max_slots);
-    const size_t lds = mdl::views_lds(max_slots, eng->maxHW, MPc, MPsc);
+    const size_t lds = mdl::views_lds(max_slots, eng->maxHW, MO, MPc, MR, MPsc);
     const int wpb = waves_per_block(lds);
     if (wpb < 1) return fail("mdl_views_features: needs %zu bytes of LDS per view", lds);
     DeviceGuard dg(eng->device);

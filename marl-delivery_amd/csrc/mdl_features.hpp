@@ -4,7 +4,8 @@
 //
 // Layout per wave (LDS, carved by feat_carve):
 //   robots  rr/rcol/rcarry/rcslot/rcell/rtgt  int32[64] each
-//   cellf   uint32[HW]   bit0 grid, bit1 wstart, bit2 atarget, bits 8.. robot count
+//   bits    uint32[5][NW] cell bitsets (NW = ceil(HW/32)): grid, robot, >=2 robots,
+//                          waiting start (ch3), active target (ch4)
 //   inv_o   uint8 [A][64]   agent a: sorted-other slot -> robot
 //   inv_p   uint16[A][MPc]  agent a: sorted-package slot -> tracker slot
 //   inv_c   uint16[MPsc]    critic: id-sorted slot -> tracker slot
@@ -18,7 +19,7 @@
 namespace mdl {
 
 struct FeatDims {
-    int A, NS, HW, MPc, MPsc;
+    int A, NS, HW, MPc, MPsc, stage;  // stage: floats of the vector staging slice
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -26,25 +27,27 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 __host__ __device__ inline size_t feat_lds_bytes(const FeatDims& d) {
     size_t s = 0;
     s += align16(sizeof(int32_t) * 64 * 6);
-    s += align16(sizeof(uint32_t) * (size_t)d.HW);
+    s += align16(sizeof(uint32_t) * 5 * (size_t)((d.HW + 31) / 32));
     s += align16((size_t)d.A * 64);
     s += align16(sizeof(uint16_t) * (size_t)d.A * (d.MPc > 0 ? d.MPc : 1));
     s += align16(sizeof(uint16_t) * (size_t)(d.MPsc > 0 ? d.MPsc : 1));
     s += align16(sizeof(uint64_t) * (size_t)(d.NS > 0 ? d.NS : 1));
     s += align16((size_t)(d.NS > 0 ? d.NS : 1));
     s += align16(sizeof(int32_t) * (size_t)(d.A + 2));
+    s += align16(sizeof(float) * (size_t)(d.stage > 0 ? d.stage : 1));
     return s;
 }
 
 struct FeatLds {
     int32_t *rr, *rcol, *rcarry, *rcslot, *rcell, *rtgt;
-    uint32_t* cellf;
+    uint32_t* bits;   // [5][NW]
     uint8_t* inv_o;
     uint16_t* inv_p;
     uint16_t* inv_c;
     uint64_t* keys;
     int8_t* scar;
     int32_t* cnt;
+    float* stage;
 };
 
 __device__ inline FeatLds feat_carve(unsigned char* base, const FeatDims& d) {
@@ -53,20 +56,23 @@ __device__ inline FeatLds feat_carve(unsigned char* base, const FeatDims& d) {
     int32_t* r = (int32_t*)(base + o);
     L.rr = r; L.rcol = r + 64; L.rcarry = r + 128; L.rcslot = r + 192; L.rcell = r + 256; L.rtgt = r + 320;
     o += align16(sizeof(int32_t) * 64 * 6);
-    L.cellf = (uint32_t*)(base + o); o += align16(sizeof(uint32_t) * (size_t)d.HW);
+    L.bits = (uint32_t*)(base + o); o += align16(sizeof(uint32_t) * 5 * (size_t)((d.HW + 31) / 32));
     L.inv_o = (uint8_t*)(base + o); o += align16((size_t)d.A * 64);
     L.inv_p = (uint16_t*)(base + o); o += align16(sizeof(uint16_t) * (size_t)d.A * (d.MPc > 0 ? d.MPc : 1));
     L.inv_c = (uint16_t*)(base + o); o += align16(sizeof(uint16_t) * (size_t)(d.MPsc > 0 ? d.MPsc : 1));
     L.keys = (uint64_t*)(base + o); o += align16(sizeof(uint64_t) * (size_t)(d.NS > 0 ? d.NS : 1));
     L.scar = (int8_t*)(base + o); o += align16((size_t)(d.NS > 0 ? d.NS : 1));
-    L.cnt = (int32_t*)(base + o);
+    L.cnt = (int32_t*)(base + o); o += align16(sizeof(int32_t) * (size_t)(d.A + 2));
+    L.stage = (float*)(base + o);
     return L;
 }
 
+enum : int { BS_GRID = 0, BS_ROBOT = 1, BS_MULTI = 2, BS_WSTART = 3, BS_ATARGET = 4 };
+
 struct FeatCtx {
-    int A, NS, H, W, HW, t, T, MO, MP, MR, MPs, MPc, MPsc;
-    const uint8_t* grid;
-    const uint16_t* rank;   // [(2H-1)][(2W-1)]
+    int A, NS, H, W, HW, NW, t, T, MO, MP, MR, MPs, MPc, MPsc;
+    const uint32_t* gridbits;  // [NW] obstacle bitset of the map
+    const uint16_t* rank;      // [(2H-1)][(2W-1)]
     float inv_hw;
 };
 
@@ -119,9 +125,21 @@ __device__ inline void feat_prepare(const Trk& trk, const FeatCtx& c, FeatLds& L
         }
         L.rtgt[lane] = tg;   // convert_observation channel 5 (MAPPO/helper.py:59-64)
     }
-    for (int i = lane; i < HW; i += WAVE) L.cellf[i] = c.grid[i] ? 1u : 0u;
+    const int NW = c.NW;
+    for (int w = lane; w < NW; w += WAVE) {
+        L.bits[BS_GRID * NW + w] = c.gridbits[w];   // host-built obstacle bitset of the map
+        L.bits[BS_ROBOT * NW + w] = 0;
+        L.bits[BS_MULTI * NW + w] = 0;
+        L.bits[BS_WSTART * NW + w] = 0;
+        L.bits[BS_ATARGET * NW + w] = 0;
+    }
     wave_sync();
-    if (lane < A) atomicAdd(&L.cellf[L.rcell[lane]], 256u);
+    if (lane < A) {
+        const int rc = L.rcell[lane];
+        const uint32_t m = 1u << (rc & 31);
+        const uint32_t old = atomicOr(&L.bits[BS_ROBOT * NW + (rc >> 5)], m);
+        if (old & m) atomicOr(&L.bits[BS_MULTI * NW + (rc >> 5)], m);   // a second robot on the cell
+    }
     for (int j0 = 0; j0 < NS; j0 += WAVE) {
         const int j = j0 + lane;
         if (j < NS && trk.present(j)) {
@@ -129,8 +147,14 @@ __device__ inline void feat_prepare(const Trk& trk, const FeatCtx& c, FeatLds& L
             const bool it = trk.in_transit(j);
             const bool wt = !it && pk_st(d) <= t;
             const int tg = pk_target(d), sc = pk_start(d);
-            if (wt) atomicOr(&L.cellf[cell_r(sc) * W + cell_c(sc)], 2u);
-            if (wt || it) atomicOr(&L.cellf[cell_r(tg) * W + cell_c(tg)], 4u);
+            if (wt) {
+                const int ci = cell_r(sc) * W + cell_c(sc);
+                atomicOr(&L.bits[BS_WSTART * NW + (ci >> 5)], 1u << (ci & 31));
+            }
+            if (wt || it) {
+                const int ci = cell_r(tg) * W + cell_c(tg);
+                atomicOr(&L.bits[BS_ATARGET * NW + (ci >> 5)], 1u << (ci & 31));
+            }
         }
     }
     // carrier of each slot: first robot (index order) carrying its id
@@ -153,13 +177,19 @@ __device__ inline void feat_prepare(const Trk& trk, const FeatCtx& c, FeatLds& L
             act = it || pk_st(trk.data(j)) <= t;
             idj = trk.id(j);
         }
-        int pos = 0;
-        for (int k = 0; k < NS; k++) {
-            const bool ak = trk.present(k) && (trk.in_transit(k) || pk_st(trk.data(k)) <= t);
-            pos += ak && trk.id(k) < idj;
+        const uint64_t b = ballot(act);
+        int pos;
+        if (Trk::kIdIndexed) {  // slot j holds id j+1: id order == slot order
+            pos = nact + popc64(b & lanemask_lt());
+        } else {
+            pos = 0;
+            for (int k = 0; k < NS; k++) {
+                const bool ak = trk.present(k) && (trk.in_transit(k) || pk_st(trk.data(k)) <= t);
+                pos += ak && trk.id(k) < idj;
+            }
         }
         if (act && pos < c.MPsc) L.inv_c[pos] = (uint16_t)j;
-        nact += popc64(ballot(act));
+        nact += popc64(b);
     }
     if (lane == 0) L.cnt[A + 1] = nact;
     wave_sync();
@@ -203,12 +233,39 @@ __device__ inline void feat_sort_agent(const Trk& trk, const FeatCtx& c, FeatLds
         np += popc64(ballot(key != ~0ull));
     }
     wave_sync();
-    for (int j0 = 0; j0 < NS; j0 += WAVE) {
-        const int j = j0 + lane;
-        const uint64_t key = j < NS ? L.keys[j] : ~0ull;
-        int pos = 0;
-        for (int k = 0; k < NS; k++) pos += L.keys[k] < key;
-        if (key != ~0ull && pos < c.MPc) L.inv_p[a * c.MPc + pos] = (uint16_t)j;
+    if (NS <= WAVE) {
+        // one chunk: keys stay in registers (lane j)
+        uint64_t key = lane < NS ? L.keys[lane] : ~0ull;
+        const int want = np < c.MPc ? np : c.MPc;
+        if (want <= 8) {
+            // selection: the `want` smallest keys by repeated wave minima (keys are unique)
+            for (int s = 0; s < want; s++) {
+                const uint32_t hi = wave_min_u32((uint32_t)(key >> 32));
+                const uint32_t lo = wave_min_u32((uint32_t)(key >> 32) == hi ? (uint32_t)key : 0xffffffffu);
+                const bool me = key == (((uint64_t)hi << 32) | lo);
+                if (me) {
+                    L.inv_p[a * c.MPc + s] = (uint16_t)lane;
+                    key = ~0ull;
+                }
+            }
+        } else {
+            // counting rank against every other key via readlane
+            int pos = 0;
+            for (int k = 0; k < NS; k++) {
+                const uint64_t kk = (uint64_t)(uint32_t)rdl((int)(uint32_t)key, k) |
+                                    ((uint64_t)(uint32_t)rdl((int)(uint32_t)(key >> 32), k) << 32);
+                pos += kk < key;
+            }
+            if (key != ~0ull && pos < c.MPc) L.inv_p[a * c.MPc + pos] = (uint16_t)lane;
+        }
+    } else {
+        for (int j0 = 0; j0 < NS; j0 += WAVE) {
+            const int j = j0 + lane;
+            const uint64_t key = j < NS ? L.keys[j] : ~0ull;
+            int pos = 0;
+            for (int k = 0; k < NS; k++) pos += L.keys[k] < key;
+            if (key != ~0ull && pos < c.MPc) L.inv_p[a * c.MPc + pos] = (uint16_t)j;
+        }
     }
     if (lane == 0) L.cnt[a] = (A - 1) | (np << 8);  // n_other | n_pkg << 8 (np <= 1024 -> use 16 bits)
     wave_sync();
@@ -221,161 +278,283 @@ __device__ __forceinline__ float dlc_over_T(int dl, int t, int T) {
     return qdiv(d, T);
 }
 
+__device__ __forceinline__ uint32_t bits_at(const FeatLds& L, int NW, int set, int cell) {
+    return (L.bits[set * NW + (cell >> 5)] >> (cell & 31)) & 1u;
+}
+
+__device__ __forceinline__ float4 float4_of_bits(uint32_t b) {
+    return make_float4((b & 1u) ? 1.0f : 0.0f, (b & 2u) ? 1.0f : 0.0f, (b & 4u) ? 1.0f : 0.0f,
+                       (b & 8u) ? 1.0f : 0.0f);
+}
+
+// one-hot of `cell` within the 4 cells starting at c0
+__device__ __forceinline__ uint32_t onehot4(int cell, int c0) {
+    const unsigned d = (unsigned)(cell - c0);
+    return d < 4u ? (1u << d) : 0u;
+}
+
+// The 4 actor-map values of plane (agent a, channel ch) at cells c0..c0+3.
+__device__ __forceinline__ uint32_t actor_bits4(const FeatLds& L, int NW, int a, int ch, int c0, bool a_valid) {
+    const int w = c0 >> 5, sh = c0 & 31;
+    const int set = ch == 0 ? BS_GRID : ch == 2 ? BS_ROBOT : ch == 3 ? BS_WSTART : BS_ATARGET;
+    const uint32_t wb = (L.bits[set * NW + w] >> sh) & 15u;
+    if (ch == 0) return wb;
+    if (!a_valid) return 0u;
+    const uint32_t own = onehot4(L.rcell[a], c0);
+    if (ch == 1) return own;
+    if (ch == 2) return (wb & ~own) | ((L.bits[BS_MULTI * NW + w] >> sh) & 15u);
+    if (ch == 5) return onehot4(L.rtgt[a], c0);
+    return wb;
+}
+
 // convert_observation for agents [a0, a0+na): dst [na][6][H][W].
 // a_valid=false reproduces the early return (channel 0 only).
-__device__ inline void emit_actor_maps(const FeatCtx& c, const FeatLds& L, int a0, int na,
-                                       bool a_valid, float* dst) {
-    const int HW = c.HW;
+__device__ inline void emit_actor_maps(const FeatCtx& c, const FeatLds& L, int a0, int na, bool a_valid, float* dst) {
+    const int HW = c.HW, NW = c.NW;
+    const int lane = lane_id();
+    if ((HW & 3) == 0 && (((uintptr_t)dst) & 15) == 0) {
+        // float4 per lane, never straddling a plane: 1 KiB per wave store
+        const int qpp = HW >> 2;
+        const float inv_qpp = 1.0f / (float)qpp;
+        const int nq = na * 6 * qpp;
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int q = lane; q < nq; q += WAVE) {
+            const int plane = fdivi(q, qpp, inv_qpp);
+            const int c0 = (q - plane * qpp) << 2;
+            const int al = plane / 6;
+            const int ch = plane - 6 * al;
+            d4[q] = float4_of_bits(actor_bits4(L, NW, a0 + al, ch, c0, a_valid));
+        }
+        return;
+    }
     const float inv_hw = c.inv_hw;
     emit(dst, na * 6 * HW, [&](int i) -> float {
         const int plane = fdivi(i, HW, inv_hw);
         const int cell = i - plane * HW;
         const int al = plane / 6;
         const int ch = plane - 6 * al;
-        const uint32_t f = L.cellf[cell];
-        if (ch == 0) return (f & 1u) ? 1.0f : 0.0f;
+        if (ch == 0) return bits_at(L, NW, BS_GRID, cell) ? 1.0f : 0.0f;
         if (!a_valid) return 0.0f;
         const int a = a0 + al;
         const int own = L.rcell[a];
         switch (ch) {
             case 1: return cell == own ? 1.0f : 0.0f;
-            case 2: return ((f >> 8) - (cell == own ? 1u : 0u)) > 0u ? 1.0f : 0.0f;
-            case 3: return (f & 2u) ? 1.0f : 0.0f;
-            case 4: return (f & 4u) ? 1.0f : 0.0f;
+            case 2: return ((bits_at(L, NW, BS_ROBOT, cell) && cell != own) || bits_at(L, NW, BS_MULTI, cell)) ? 1.0f
+                                                                                                                : 0.0f;
+            case 3: return bits_at(L, NW, BS_WSTART, cell) ? 1.0f : 0.0f;
+            case 4: return bits_at(L, NW, BS_ATARGET, cell) ? 1.0f : 0.0f;
             default: return cell == L.rtgt[a] ? 1.0f : 0.0f;
         }
     });
 }
 
-// convert_global_state map: dst [4][H][W]
+// convert_global_state map: dst [4][H][W] (grid, robots, waiting starts, active targets)
 __device__ inline void emit_critic_map(const FeatCtx& c, const FeatLds& L, float* dst) {
-    const int HW = c.HW;
+    const int HW = c.HW, NW = c.NW;
+    const int lane = lane_id();
+    if ((HW & 3) == 0 && (((uintptr_t)dst) & 15) == 0) {
+        const int qpp = HW >> 2;
+        const float inv_qpp = 1.0f / (float)qpp;
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int q = lane; q < 4 * qpp; q += WAVE) {
+            const int ch = fdivi(q, qpp, inv_qpp);
+            const int c0 = (q - ch * qpp) << 2;
+            const int set = ch == 0 ? BS_GRID : ch == 1 ? BS_ROBOT : ch == 2 ? BS_WSTART : BS_ATARGET;
+            d4[q] = float4_of_bits((L.bits[set * NW + (c0 >> 5)] >> (c0 & 31)) & 15u);
+        }
+        return;
+    }
     const float inv_hw = c.inv_hw;
     emit(dst, 4 * HW, [&](int i) -> float {
         const int ch = fdivi(i, HW, inv_hw);
-        const uint32_t f = L.cellf[i - ch * HW];
-        switch (ch) {
-            case 0: return (f & 1u) ? 1.0f : 0.0f;
-            case 1: return (f >> 8) ? 1.0f : 0.0f;
-            case 2: return (f & 2u) ? 1.0f : 0.0f;
-            default: return (f & 4u) ? 1.0f : 0.0f;
-        }
+        const int cell = i - ch * HW;
+        const int set = ch == 0 ? BS_GRID : ch == 1 ? BS_ROBOT : ch == 2 ? BS_WSTART : BS_ATARGET;
+        return bits_at(L, NW, set, cell) ? 1.0f : 0.0f;
     });
+}
+
+// generate_vector_features value of agent a, output index f (MAPPO/helper.py:68-165)
+template <class Trk>
+__device__ inline float actor_value(const Trk& trk, const FeatCtx& c, const FeatLds& L, int a, int f) {
+    const int H = c.H, W = c.W, t = c.t, T = c.T;
+    const int o_end = 6 + 5 * c.MO, p_end = o_end + 5 * c.MP;
+    const int ra = L.rr[a], ca = L.rcol[a];
+    if (f < 6) {
+        if (f == 0) return qdiv(ra, H);
+        if (f == 1) return qdiv(ca, W);
+        const int cy = L.rcarry[a];
+        if (f == 2) return cy != 0 ? 1.0f : 0.0f;
+        const int cs = L.rcslot[a];
+        if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
+        const uint64_t d = trk.data(cs);
+        const int tg = pk_target(d);
+        if (f == 3) return qdiv(cell_r(tg) - ra, H);
+        if (f == 4) return qdiv(cell_c(tg) - ca, W);
+        return dlc_over_T(pk_dl(d), t, T);
+    }
+    if (f < o_end) {
+        const int s = fdivi(f - 6, 5, 0.2f);
+        const int k = f - 6 - 5 * s;
+        if (s >= (L.cnt[a] & 0xff)) return 0.0f;
+        const int o = L.inv_o[a * 64 + s];
+        const int ro = L.rr[o], co = L.rcol[o];
+        if (k == 0) return qdiv(ro - ra, H);
+        if (k == 1) return qdiv(co - ca, W);
+        const int cy = L.rcarry[o];
+        if (k == 2) return cy != 0 ? 1.0f : 0.0f;
+        const int cs = L.rcslot[o];
+        if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
+        const int tg = pk_target(trk.data(cs));
+        if (k == 3) return qdiv(cell_r(tg) - ro, H);
+        return qdiv(cell_c(tg) - co, W);
+    }
+    if (f < p_end) {
+        const int s = fdivi(f - o_end, 5, 0.2f);
+        const int k = f - o_end - 5 * s;
+        if (s >= (L.cnt[a] >> 8) || s >= c.MPc) return 0.0f;
+        const int j = L.inv_p[a * c.MPc + s];
+        const uint64_t d = trk.data(j);
+        const int sc = pk_start(d), tg = pk_target(d);
+        switch (k) {
+            case 0: return qdiv(cell_r(sc) - ra, H);
+            case 1: return qdiv(cell_c(sc) - ca, W);
+            case 2: return qdiv(cell_r(tg) - ra, H);
+            case 3: return qdiv(cell_c(tg) - ca, W);
+            default: return dlc_over_T(pk_dl(d), t, T);
+        }
+    }
+    return T > 0 ? qdiv(t, T) : 0.0f;
+}
+
+// convert_global_state vector value at output index f (MAPPO/helper.py:199-255)
+template <class Trk>
+__device__ inline float critic_value(const Trk& trk, const FeatCtx& c, const FeatLds& L, int f) {
+    const int H = c.H, W = c.W, t = c.t, T = c.T, A = c.A, MR = c.MR;
+    const int r_end = 6 * MR, p_end = r_end + 7 * c.MPs;
+    if (f < r_end) {
+        const int i = fdivi(f, 6, 1.0f / 6.0f);
+        const int k = f - 6 * i;
+        if (i >= A) return 0.0f;
+        if (k == 0) return qdiv(L.rr[i], H);
+        if (k == 1) return qdiv(L.rcol[i], W);
+        const int cy = L.rcarry[i];
+        if (k == 2) return cy != 0 ? 1.0f : 0.0f;
+        const int cs = L.rcslot[i];
+        if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
+        const uint64_t d = trk.data(cs);
+        const int tg = pk_target(d);
+        if (k == 3) return qdiv(cell_r(tg), H);
+        if (k == 4) return qdiv(cell_c(tg), W);
+        return dlc_over_T(pk_dl(d), t, T);
+    }
+    if (f < p_end) {
+        const int s = fdivi(f - r_end, 7, 1.0f / 7.0f);
+        const int k = f - r_end - 7 * s;
+        if (s >= L.cnt[A + 1] || s >= c.MPsc) return 0.0f;
+        const int j = L.inv_c[s];
+        const uint64_t d = trk.data(j);
+        const bool waiting = !trk.in_transit(j);
+        const int sc = pk_start(d), tg = pk_target(d);
+        switch (k) {
+            case 0: return waiting ? qdiv(cell_r(sc), H) : 0.0f;
+            case 1: return waiting ? qdiv(cell_c(sc), W) : 0.0f;
+            case 2: return qdiv(cell_r(tg), H);
+            case 3: return qdiv(cell_c(tg), W);
+            case 4: return dlc_over_T(pk_dl(d), t, T);
+            case 5: return waiting ? 0.0f : 1.0f;
+            default: {
+                if (waiting) return -1.0f;
+                const int car = L.scar[j];
+                if (car < 0) return -1.0f;
+                return MR > 1 ? qdiv(car, MR - 1) : 0.0f;
+            }
+        }
+    }
+    return T > 0 ? qdiv(t, T) : 0.0f;
+}
+
+// Vector outputs are mostly padding.  Stage every slot that can be non-zero
+// (compact layout, one value per lane per pass, so each division runs once
+// with all lanes busy), then stream the full row: padding as literal zeros,
+// the rest read back from the staging slice.
+__host__ __device__ inline int actor_compact_dim(int A, int MO, int MPc) {
+    const int MOc = MO < A - 1 ? MO : (A - 1 > 0 ? A - 1 : 0);
+    return 6 + 5 * MOc + 5 * MPc + 1;
+}
+__host__ __device__ inline int critic_compact_dim(int A, int MR, int MPsc) {
+    return 6 * (A < MR ? A : MR) + 7 * MPsc + 1;
+}
+// agents whose compact actor rows are staged together (<= 2048 floats, >= 1 agent)
+__host__ __device__ inline int actor_group(int na, int Dc) {
+    const int g = 2048 / Dc;
+    return g < 1 ? 1 : (g < na ? g : na);
 }
 
 // generate_vector_features for agents [a0, a0+na): dst [na][6+5MO+5MP+1]
 template <class Trk>
 __device__ inline void emit_actor_vecs(const Trk& trk, const FeatCtx& c, const FeatLds& L, int a0, int na,
                                        bool a_valid, float* dst) {
+    const int lane = lane_id();
     const int Dv = 6 + 5 * c.MO + 5 * c.MP + 1;
-    const float inv_dv = 1.0f / (float)Dv;
-    const int H = c.H, W = c.W, t = c.t, T = c.T;
+    if (!a_valid) {
+        emit(dst, na * Dv, [](int) -> float { return 0.0f; });
+        return;
+    }
+    const int MOc = c.MO < c.A - 1 ? c.MO : (c.A - 1 > 0 ? c.A - 1 : 0);
+    const int o_c = 6 + 5 * MOc, p_c = o_c + 5 * c.MPc;   // compact section ends
+    const int Dc = p_c + 1;
     const int o_end = 6 + 5 * c.MO, p_end = o_end + 5 * c.MP;
-    emit(dst, na * Dv, [&](int i) -> float {
-        if (!a_valid) return 0.0f;
-        const int al = fdivi(i, Dv, inv_dv);
-        const int f = i - al * Dv;
-        const int a = a0 + al;
-        const int ra = L.rr[a], ca = L.rcol[a];
-        if (f < 6) {
-            if (f == 0) return qdiv(ra, H);
-            if (f == 1) return qdiv(ca, W);
-            const int cy = L.rcarry[a];
-            if (f == 2) return cy != 0 ? 1.0f : 0.0f;
-            const int cs = L.rcslot[a];
-            if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
-            const uint64_t d = trk.data(cs);
-            const int tg = pk_target(d);
-            if (f == 3) return qdiv(cell_r(tg) - ra, H);
-            if (f == 4) return qdiv(cell_c(tg) - ca, W);
-            return dlc_over_T(pk_dl(d), t, T);
+    const float inv_dc = 1.0f / (float)Dc, inv_dv = 1.0f / (float)Dv;
+    const int G = actor_group(na, Dc);   // agents staged per pass
+    for (int g0 = 0; g0 < na; g0 += G) {
+        const int ng = na - g0 < G ? na - g0 : G;
+        for (int ci = lane; ci < ng * Dc; ci += WAVE) {
+            const int al = fdivi(ci, Dc, inv_dc);
+            const int cf = ci - al * Dc;
+            const int f = cf < o_c ? cf : cf < p_c ? o_end + (cf - o_c) : Dv - 1;
+            L.stage[ci] = actor_value(trk, c, L, a0 + g0 + al, f);
         }
-        if (f < o_end) {
-            const int s = fdivi(f - 6, 5, 0.2f);
-            const int k = f - 6 - 5 * s;
-            const int cnt = L.cnt[a];
-            if (s >= (cnt & 0xff)) return 0.0f;
-            const int o = L.inv_o[a * 64 + s];
-            const int ro = L.rr[o], co = L.rcol[o];
-            if (k == 0) return qdiv(ro - ra, H);
-            if (k == 1) return qdiv(co - ca, W);
-            const int cy = L.rcarry[o];
-            if (k == 2) return cy != 0 ? 1.0f : 0.0f;
-            const int cs = L.rcslot[o];
-            if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
-            const int tg = pk_target(trk.data(cs));
-            if (k == 3) return qdiv(cell_r(tg) - ro, H);
-            return qdiv(cell_c(tg) - co, W);
-        }
-        if (f < p_end) {
-            const int s = fdivi(f - o_end, 5, 0.2f);
-            const int k = f - o_end - 5 * s;
-            const int npk = L.cnt[a] >> 8;
-            if (s >= npk || s >= c.MPc) return 0.0f;
-            const int j = L.inv_p[a * c.MPc + s];
-            const uint64_t d = trk.data(j);
-            const int sc = pk_start(d), tg = pk_target(d);
-            switch (k) {
-                case 0: return qdiv(cell_r(sc) - ra, H);
-                case 1: return qdiv(cell_c(sc) - ca, W);
-                case 2: return qdiv(cell_r(tg) - ra, H);
-                case 3: return qdiv(cell_c(tg) - ca, W);
-                default: return dlc_over_T(pk_dl(d), t, T);
-            }
-        }
-        return T > 0 ? qdiv(t, T) : 0.0f;
-    });
+        wave_sync();
+        emit(dst + (size_t)g0 * Dv, ng * Dv, [&](int i) -> float {
+            const int al = fdivi(i, Dv, inv_dv);
+            const int f = i - al * Dv;
+            int cf;
+            if (f < o_c) cf = f;
+            else if (f < o_end) return 0.0f;
+            else if (f < o_end + 5 * c.MPc) cf = o_c + (f - o_end);
+            else if (f < p_end) return 0.0f;
+            else cf = Dc - 1;
+            return L.stage[al * Dc + cf];
+        });
+        wave_sync();
+    }
 }
 
 // convert_global_state vector: dst [6MR+7MPs+1]
 template <class Trk>
 __device__ inline void emit_critic_vec(const Trk& trk, const FeatCtx& c, const FeatLds& L, float* dst) {
+    const int lane = lane_id();
     const int Dg = 6 * c.MR + 7 * c.MPs + 1;
-    const int H = c.H, W = c.W, t = c.t, T = c.T, A = c.A, MR = c.MR;
-    const int r_end = 6 * MR, p_end = r_end + 7 * c.MPs;
-    const int nact = L.cnt[A + 1];
+    const int r_end = 6 * c.MR, p_end = r_end + 7 * c.MPs;
+    const int nact = L.cnt[c.A + 1];
+    const int r_c = 6 * (c.A < c.MR ? c.A : c.MR);                 // robot rows present
+    const int np = nact < c.MPsc ? nact : c.MPsc;
+    const int p_c = r_c + 7 * np;                                    // package rows present
+    for (int ci = lane; ci <= p_c; ci += WAVE) {
+        const int f = ci < r_c ? ci : ci < p_c ? r_end + (ci - r_c) : Dg - 1;
+        L.stage[ci] = critic_value(trk, c, L, f);
+    }
+    wave_sync();
     emit(dst, Dg, [&](int f) -> float {
-        if (f < r_end) {
-            const int i = fdivi(f, 6, 1.0f / 6.0f);
-            const int k = f - 6 * i;
-            if (i >= A) return 0.0f;
-            if (k == 0) return qdiv(L.rr[i], H);
-            if (k == 1) return qdiv(L.rcol[i], W);
-            const int cy = L.rcarry[i];
-            if (k == 2) return cy != 0 ? 1.0f : 0.0f;
-            const int cs = L.rcslot[i];
-            if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
-            const uint64_t d = trk.data(cs);
-            const int tg = pk_target(d);
-            if (k == 3) return qdiv(cell_r(tg), H);
-            if (k == 4) return qdiv(cell_c(tg), W);
-            return dlc_over_T(pk_dl(d), t, T);
-        }
-        if (f < p_end) {
-            const int s = fdivi(f - r_end, 7, 1.0f / 7.0f);
-            const int k = f - r_end - 7 * s;
-            if (s >= nact || s >= c.MPsc) return 0.0f;
-            const int j = L.inv_c[s];
-            const uint64_t d = trk.data(j);
-            const bool waiting = !trk.in_transit(j);
-            const int sc = pk_start(d), tg = pk_target(d);
-            switch (k) {
-                case 0: return waiting ? qdiv(cell_r(sc), H) : 0.0f;
-                case 1: return waiting ? qdiv(cell_c(sc), W) : 0.0f;
-                case 2: return qdiv(cell_r(tg), H);
-                case 3: return qdiv(cell_c(tg), W);
-                case 4: return dlc_over_T(pk_dl(d), t, T);
-                case 5: return waiting ? 0.0f : 1.0f;
-                default: {
-                    if (waiting) return -1.0f;
-                    const int car = L.scar[j];
-                    if (car < 0) return -1.0f;
-                    return MR > 1 ? qdiv(car, MR - 1) : 0.0f;
-                }
-            }
-        }
-        return T > 0 ? qdiv(t, T) : 0.0f;
+        int cf;
+        if (f < r_c) cf = f;
+        else if (f < r_end) return 0.0f;
+        else if (f < r_end + 7 * np) cf = r_c + (f - r_end);
+        else if (f < p_end) return 0.0f;
+        else cf = p_c;
+        return L.stage[cf];
     });
+    wave_sync();
 }
 
 }  // namespace mdl

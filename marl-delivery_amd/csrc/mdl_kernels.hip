@@ -22,6 +22,13 @@
 
 namespace mdl {
 
+// floats of the vector staging slice: max(actor rows of `na` agents, critic row)
+__host__ __device__ inline int stage_floats(int A, int na, int MO, int MPc, int MR, int MPsc) {
+    const int dc = actor_compact_dim(A, MO, MPc);
+    const int a = actor_group(na, dc) * dc, cr = critic_compact_dim(A, MR, MPsc);
+    return a > cr ? a : cr;
+}
+
 // --------------------------------------------------------------- reset LDS
 struct ResetLds {
     uint64_t* pk;       // [P] new package table
@@ -100,17 +107,6 @@ __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[N
     }
 }
 
-// min over lanes of v (< 1024) where valid; 1023 if none.  Ballot bisection.
-__device__ __forceinline__ int wave_min10(bool valid, int v) {
-    int m = 0;
-#pragma unroll
-    for (int b = 9; b >= 0; b--) {
-        const bool cand = valid && ((v >> b) == (m >> b));
-        if (ballot(cand) == 0) m |= 1 << b;
-    }
-    return m;
-}
-
 // ------------------------------------------------------------------ seed
 __global__ __launch_bounds__(256) void k_seed(DevParams p, const uint32_t* __restrict__ seeds, int wpb,
                                               int lds_stride) {
@@ -130,7 +126,8 @@ __global__ __launch_bounds__(256) void k_seed(DevParams p, const uint32_t* __res
     }
     wave_sync();
     const int cell = do_reset(p, e, md, L, true);
-    if (lane < p.A) p.rob[(size_t)e * p.A + lane] = (uint32_t)cell;
+    if (lane < p.A)
+        p.rob[(size_t)e * p.A + lane] = rob_pack(cell, 0, p.movevalid[md.grid_off + cell_r(cell) * md.W + cell_c(cell)]);
     for (int j = lane; j < p.P; j += WAVE) {
         const size_t g = (size_t)e * p.P + j;
         p.pkg[g] = L.pk[j];
@@ -184,7 +181,8 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restric
         dirty[c] = false;
     }
     if (p.stale) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, 0, 0, ctr);
-    if (lane < A) p.rob[(size_t)e * A + lane] = (uint32_t)cell;
+    if (lane < A)
+        p.rob[(size_t)e * A + lane] = rob_pack(cell, 0, p.movevalid[md.grid_off + cell_r(cell) * md.W + cell_c(cell)]);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
@@ -262,7 +260,8 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     }
     int mv = MV_S, op = 0;
     if (act) decode_action(araw, fmt, mv, op);
-    int cell = (int)(rv & 0xffffu), carry = (int)(rv >> 16);
+    int cell = rob_cell(rv), carry = rob_carry(rv);
+    uint32_t vmask = rob_valid(rv);
     const int t0 = es.t;
     // tracker_prev view: data / iteration order per slot
 #pragma unroll
@@ -281,11 +280,8 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     // loop, checked against the oracle's literal restatement.
     const int pcell = cell, pcarry = carry;
     int prop = cell;
-    if (act && mv >= MV_L && mv <= MV_D) {
-        const int ci = cell_r(cell) * md.W + cell_c(cell);
-        const uint32_t vm = p.movevalid[md.grid_off + ci];
-        if ((vm >> mv) & 1u) prop = cell + (mv == MV_L ? -256 : mv == MV_R ? 256 : mv == MV_U ? -1 : 1);
-    }
+    if (act && ((vmask >> mv) & 1u))   // bits 1..4 only: S / other moves never move
+        prop = cell + (mv == MV_L ? -256 : mv == MV_R ? 256 : mv == MV_U ? -1 : 1);
     const bool mover = act && prop != cell;
     const uint64_t movers = ballot(mover);
     uint64_t moved = 0;
@@ -304,7 +300,10 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             if (nm == moved) break;
             moved = nm;
         }
-        if ((moved >> lane) & 1ull) cell = prop;
+        if ((moved >> lane) & 1ull) {
+            cell = prop;
+            vmask = p.movevalid[md.grid_off + cell_r(cell) * md.W + cell_c(cell)];  // consumed at write-back
+        }
     }
     const int n_cost = popc64(moved);
 
@@ -427,7 +426,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
                     if (need_can) can |= ballot(wprev[c] && sc == cc) != 0;
                     if (need_idle) idle |= ballot(wprev[c] && dist[c] <= 3) != 0;
                     if (need_near) {
-                        const int m = wave_min10(wprev[c], dist[c]);
+                        const int m = (int)wave_min_u32(wprev[c] ? (uint32_t)dist[c] : 1023u);
                         dmin = m < dmin ? m : dmin;
                     }
                 }
@@ -437,17 +436,16 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
 #pragma unroll
                     for (int c = 0; c < NCH; c++) {
                         uint64_t tie = ballot(wprev[c] && dist[c] == dmin);
+                        if (!STALE && best_o != 0xffffffffu) tie = 0;  // fresh: order == id, first tie wins
                         while (tie) {
                             const int jj = ffs64(tie);
-                            tie &= tie - 1;
+                            tie = STALE ? (tie & (tie - 1)) : 0ull;
                             const uint32_t o = (uint32_t)rdl((int)tq[c], jj);
                             if (o < best_o) {
                                 best_o = o;
                                 near_cell = rdl(pk_start(td[c]), jj);
                             }
-                            if (!STALE) break;  // fresh: order == id, the first tie wins
                         }
-                        if (!STALE && best_o != 0xffffffffu) break;
                     }
                 }
             }
@@ -489,6 +487,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         if (act) {
             cell = nc;
             carry = 0;
+            vmask = p.movevalid[md.grid_off + cell_r(cell) * md.W + cell_c(cell)];
         }
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
@@ -503,7 +502,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     }
 
     // ---- write back only what changed ----
-    if (act) p.rob[(size_t)e * A + lane] = (uint32_t)cell | ((uint32_t)carry << 16);
+    if (act) p.rob[(size_t)e * A + lane] = rob_pack(cell, carry, vmask);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
@@ -565,20 +564,21 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
     }
     const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
     FeatCtx c;
-    c.A = A; c.NS = P; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.t = p.es[e].t; c.T = p.obsT;
+    c.A = A; c.NS = P; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.NW = (c.HW + 31) / 32;
+    c.t = p.es[e].t; c.T = p.obsT;
     c.MO = p.MO; c.MP = p.MP; c.MR = p.MR; c.MPs = p.MPs;
     c.MPc = p.MP < P ? p.MP : P;
     c.MPsc = p.MPs < P ? p.MPs : P;
-    c.grid = p.grids + md.grid_off;
+    c.gridbits = p.gridbits + md.bits_off;
     c.rank = p.rank + md.rank_off;
     c.inv_hw = md.inv_hw;
-    FeatDims fd{A, P, c.HW, c.MPc, c.MPsc};
+    FeatDims fd{A, P, c.HW, c.MPc, c.MPsc, stage_floats(A, A, c.MO, c.MPc, c.MR, c.MPsc)};
     FeatLds L = feat_carve(base + obs_pre_bytes(P), fd);
 
     const bool act = lane < A;
     const uint32_t rv = act ? p.rob[(size_t)e * A + lane] : 0u;
-    const int cell = (int)(rv & 0xffffu);
-    const int carry = (int)(rv >> 16);
+    const int cell = rob_cell(rv);
+    const int carry = rob_carry(rv);
     for (int j = lane; j < P; j += WAVE) {
         const size_t g = (size_t)e * P + j;
         const uint64_t d = p.pkg[g];
@@ -687,12 +687,12 @@ __global__ __launch_bounds__(256) void k_views_features(DevParams p, const int32
     const TrkView trk = load_view(views + offs[w], V, t, A, map, cell, carry);
     const MapDesc md = p.maps[map];
     FeatCtx c;
-    c.A = A; c.NS = trk.n; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.t = t; c.T = T;
+    c.A = A; c.NS = trk.n; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.NW = (c.HW + 31) / 32; c.t = t; c.T = T;
     c.MO = MO; c.MP = MP; c.MR = MR; c.MPs = MPs; c.MPc = MPc; c.MPsc = MPsc;
-    c.grid = p.grids + md.grid_off;
+    c.gridbits = p.gridbits + md.bits_off;
     c.rank = p.rank + md.rank_off;
     c.inv_hw = md.inv_hw;
-    FeatDims fd{64, NSmax, HW, MPc, MPsc};
+    FeatDims fd{64, NSmax, HW, MPc, MPsc, stage_floats(64, 1, MO, MPc, MR, MPsc)};
     FeatLds L = feat_carve(base + view_pre_bytes(NSmax), fd);
     feat_prepare(trk, c, L, cell, carry);
     const int a = agent_idx ? agent_idx[w] : 0;
@@ -750,9 +750,9 @@ __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict
     if (robots && lane < A) {
         const uint32_t rv = p.rob[(size_t)e * A + lane];
         int32_t* o = robots + ((size_t)e * A + lane) * 3;
-        o[0] = cell_r((int)(rv & 0xffffu));
-        o[1] = cell_c((int)(rv & 0xffffu));
-        o[2] = (int)(rv >> 16);
+        o[0] = cell_r(rob_cell(rv));
+        o[1] = cell_c(rob_cell(rv));
+        o[2] = rob_carry(rv);
     }
     for (int j = lane; j < P; j += WAVE) {
         const size_t g = (size_t)e * P + j;
@@ -898,12 +898,13 @@ hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int
 }
 
 size_t step_lds(int P) { return reset_lds_bytes(P); }
-size_t obs_lds(int A, int P, int HW, int MP, int MPs) {
-    FeatDims d{A, P, HW, MP < P ? MP : P, MPs < P ? MPs : P};
+size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs) {
+    const int MPc = MP < P ? MP : P, MPsc = MPs < P ? MPs : P;
+    FeatDims d{A, P, HW, MPc, MPsc, stage_floats(A, A, MO, MPc, MR, MPsc)};
     return obs_pre_bytes(P) + feat_lds_bytes(d);
 }
-size_t views_lds(int NSmax, int HW, int MPc, int MPsc) {
-    FeatDims d{64, NSmax, HW, MPc, MPsc};
+size_t views_lds(int NSmax, int HW, int MO, int MPc, int MR, int MPsc) {
+    FeatDims d{64, NSmax, HW, MPc, MPsc, stage_floats(64, 1, MO, MPc, MR, MPsc)};
     return view_pre_bytes(NSmax) + feat_lds_bytes(d);
 }
 size_t views_shaped_lds(int NSmax) { return view_pre_bytes(NSmax); }

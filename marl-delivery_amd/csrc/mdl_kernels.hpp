@@ -27,8 +27,8 @@ hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int
                          int32_t* tracker, int32_t* tracker_data, hipStream_t s);
 
 size_t step_lds(int P);
-size_t obs_lds(int A, int P, int HW, int MP, int MPs);
-size_t views_lds(int NSmax, int HW, int MPc, int MPsc);
+size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs);
+size_t views_lds(int NSmax, int HW, int MO, int MPc, int MR, int MPsc);
 size_t views_shaped_lds(int NSmax);
 
 }  // namespace mdl

@@ -1,0 +1,109 @@
+"""Secondary measurements for BASELINE.json configs 3-5 (single GPU slices).
+
+  --config 3   map1, A=5, E=16384: step + full observation build every step
+               (actor 6ch map + vector 52 (MO=4, MP=5), critic 4ch map + vector 1301)
+  --config 3b  as 3 with the 1007-dim actor vector (MO=MP=100)
+  --config 4   map1..map5 mixed, A=5, E=65536/8 per GPU (one GPU's shard), step only
+  --config 5   synthetic 64x64, A=16, P=100, E=131072/8 per GPU, step only
+
+Prints one JSON line per config with per-kernel HIP-event times and the
+algorithmic-bytes roofline of SURVEY.md §8(d).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "marl-delivery_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM = 8000.0
+
+
+def timed(fn, n):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for k in range(n):
+        fn(k)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e3  # us per call
+
+
+def run(cfg, steps, warmup):
+    import marl_gpu
+    from marl_gpu.maps import grid_array, load_map, map_path
+    dev = torch.device("cuda", 0)
+    if cfg in ("3", "3b"):
+        E, A, P, T = 16384, 5, 50, 500
+        mo, mp = (4, 5) if cfg == "3" else (100, 100)
+        env = marl_gpu.BatchedEnv(grid_array(load_map(map_path("map1.txt"))), E, A, P, T, seed=42, tracker="mappo",
+                                  max_other_robots=mo, max_packages_obs=mp)
+        groups = [(0, E)]
+    elif cfg == "4":
+        E, A, P, T = 65536 // 8, 5, 50, 500
+        maps = [grid_array(load_map(map_path(f"map{i}.txt"))) for i in range(1, 6)]
+        sizes = [E // 5 + (1 if i < E % 5 else 0) for i in range(5)]
+        env_map = np.concatenate([np.full(s, i) for i, s in enumerate(sizes)])
+        env = marl_gpu.BatchedEnv(maps, E, A, P, T, seed=42, env_map=env_map, tracker="mappo", max_packages_obs=5)
+        starts = np.cumsum([0] + sizes)
+        groups = [(int(starts[i]), int(sizes[i])) for i in range(5)]
+    else:
+        E, A, P, T = 131072 // 8, 16, 100, 500
+        env = marl_gpu.BatchedEnv(grid_array(load_map(map_path("synthetic64.txt"))), E, A, P, T, seed=7,
+                                  tracker="mappo", max_other_robots=15, max_packages_obs=20, max_robots_state=16,
+                                  max_packages_state=100)
+        groups = [(0, E)]
+    env.reset()
+    gen = torch.Generator(device=dev).manual_seed(0)
+    G = 50
+    acts = torch.randint(0, 15, (G, E, A), generator=gen, device=dev, dtype=torch.int32).to(torch.uint8)
+    out = {}
+    bufs = None
+    if cfg in ("3", "3b"):
+        bufs = env.obs_buffers()
+    for k in range(warmup):
+        env.step(acts[k % G])
+    step_us = timed(lambda k: env.step(acts[k % G]), steps)
+    out["step_us"] = step_us
+    out["agent_steps_per_s_step_only"] = E * A / (step_us * 1e-6)
+    step_bytes = (9 * A + 10 * P + 41) * E
+    out["step_roofline"] = {"achieved_GBs": step_bytes / (step_us * 1e-6) / 1e9, "frac": step_bytes / (step_us * 1e-6) / 1e9 / HBM}
+    if bufs is not None:
+        for k in range(3):
+            env.build_obs(out=bufs)
+        obs_us = timed(lambda k: env.build_obs(out=bufs), max(20, steps // 5))
+        H = W = 10
+        obs_bytes = E * 4 * (A * 6 * H * W + A * env.actor_vec_dim + 4 * H * W + env.critic_vec_dim)
+        out["obs_us"] = obs_us
+        out["obs_write_bytes"] = obs_bytes
+        out["obs_roofline"] = {"achieved_GBs": obs_bytes / (obs_us * 1e-6) / 1e9,
+                               "frac": obs_bytes / (obs_us * 1e-6) / 1e9 / HBM}
+        both = timed(lambda k: (env.step(acts[k % G]), env.build_obs(out=bufs)), max(20, steps // 5))
+        out["step_plus_obs_us"] = both
+        out["agent_steps_per_s_with_obs"] = E * A / (both * 1e-6)
+    out.update(config=cfg, envs=E, agents=A, packages=P, T=T, groups=groups)
+    print(json.dumps(out), flush=True)
+    env.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="3,3b,4,5")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    for c in a.config.split(","):
+        run(c, a.steps, a.warmup)
+
+
+if __name__ == "__main__":
+    main()

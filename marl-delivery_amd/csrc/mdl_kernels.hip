@@ -20,6 +20,12 @@
 #include "mdl_kernels.hpp"
 #include "mdl_features.hpp"
 
+// Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
+// reward, 2 the tracker update, 4 movement, 8 package actions.  0 in the product.
+#ifndef MDL_ABLATE
+#define MDL_ABLATE 0
+#endif
+
 namespace mdl {
 
 // floats of the vector staging slice: max(actor rows of `na` agents, critic row)
@@ -282,7 +288,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     int prop = cell;
     if (act && ((vmask >> mv) & 1u))   // bits 1..4 only: S / other moves never move
         prop = cell + (mv == MV_L ? -256 : mv == MV_R ? 256 : mv == MV_U ? -1 : 1);
-    const bool mover = act && prop != cell;
+    const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
     const uint64_t movers = ballot(mover);
     uint64_t moved = 0;
     if (movers) {
@@ -309,7 +315,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
 
     // ---- package actions (env.py:259-292); robots sit on distinct cells, so
     // pick-ups and drops of different robots never interact ----
-    uint64_t pickers = ballot(act && op == 1 && carry == 0);
+    uint64_t pickers = ballot(!(MDL_ABLATE & 8) && act && op == 1 && carry == 0);
     while (pickers) {
         const int i = ffs64(pickers);
         pickers &= pickers - 1;
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         }
         if (found >= 0 && lane == i) carry = found + 1;
     }
-    uint64_t droppers = ballot(act && op == 2 && carry != 0);
+    uint64_t droppers = ballot(!(MDL_ABLATE & 8) && act && op == 2 && carry != 0);
     uint64_t dmask = 0, omask = 0;
     while (droppers) {
         const int i = ffs64(droppers);
@@ -372,103 +378,114 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     const bool done = (t1 == p.T) || (ndel == P);
 
     // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
+    // Agents on lanes (VALU work); one wave-uniform pass over the waiting
+    // packages of tracker_prev (st <= t_prev) serves every agent's
+    // can-pick-up / idle-nearby / nearest-target query.
     float s_lane = 0.0f;
-    {
+    if (!(MDL_ABLATE & 1)) {
         const float* C = p.shaping;
-        bool wprev[NCH];
+        // tracker_prev entry of each agent's previously carried id (ds_bpermute gather)
+        const int pj = pcarry - 1;
+        uint32_t pf = 0;
+        uint64_t pdat = 0;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const int src = (pj & 63) << 2;
+            const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ps0[c]);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)td[c]);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(td[c] >> 32));
+            if ((pj >> 6) == c) {
+                pf = f;
+                pdat = (uint64_t)lo | ((uint64_t)hi << 32);
+            }
+        }
+        const bool ppres = act && pcarry != 0 && pcarry <= P &&
+                           (STALE ? (pf & PS_PRESENT) != 0
+                                  : ((pf & PS_STATUS) == ST_WAITING || (pf & PS_STATUS) == ST_IN_TRANSIT));
+        // Per agent (uniform loop): distances on the package lanes, answers
+        // by ballot (can pick up here / idle next to a package) and DPP
+        // minima (nearest waiting package, ties by tracker iteration order);
+        // results land on the agent's lane.
+        bool wv[NCH];
+        int stc[NCH];
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const uint32_t f = ps0[c];
             const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
-            wprev[c] = waiting && pk_st(td[c]) <= t0;
+            wv[c] = waiting && pk_st(td[c]) <= t0;
+            stc[c] = pk_start(td[c]);
         }
-        for (int a = 0; a < A; a++) {
-            const int pc = rdl(pcell, a), pcy = rdl(pcarry, a);
-            const int cc = rdl(cell, a), ccy = rdl(carry, a);
-            const int mva = rdl(mv, a), opa = rdl(op, a);
-            bool ppres = false;
-            uint64_t pdata = 0;
-            if (pcy != 0 && pcy <= P) {
-                const int j = pcy - 1, c2 = j >> 6, jj = j & 63;
-                uint32_t f = 0;
-                uint64_t d = 0;
+        uint64_t anyw = 0;
 #pragma unroll
-                for (int c = 0; c < NCH; c++)
-                    if (c == c2) {
-                        f = ps0[c];
-                        d = td[c];
-                    }
-                f = (uint32_t)rdl((int)f, jj);
-                d = (uint64_t)(uint32_t)rdl((int)(uint32_t)d, jj) |
-                    ((uint64_t)(uint32_t)rdl((int)(uint32_t)(d >> 32), jj) << 32);
-                ppres = STALE ? (f & PS_PRESENT) != 0
-                              : ((f & PS_STATUS) == ST_WAITING || (f & PS_STATUS) == ST_IN_TRANSIT);
-                pdata = d;
-            }
-            float s = 0.0f;
-            // 1. pickup / delivery
-            if (pcy == 0 && ccy != 0) s = s + C[SH_PICK];
-            else if (pcy != 0 && ccy == 0 && ppres && cc == pk_target(pdata))
-                s = s + ((t1 <= pk_dl(pdata)) ? C[SH_ONTIME] : C[SH_LATE]);
-            const bool moved_a = pc != cc;
-            const bool need_can = opa == 1 && pcy == 0 && ccy == 0;
-            const bool need_idle = !moved_a && mva == MV_S && pcy == 0;
-            const bool need_near = moved_a && !(pcy != 0 && ppres);
-            bool can = false, idle = false;
-            int near_cell = -1;
-            if (need_can || need_idle || need_near) {
-                int dmin = 1023;
+        for (int c = 0; c < NCH; c++) anyw |= ballot(wv[c]);
+        bool can = false, idle = false;
+        int best_cell = -1;
+        if (anyw) {
+            for (int a = 0; a < A; a++) {
+                const int pa = rdl(pcell, a), ca = rdl(cell, a);
+                bool can_a = false, idle_a = false;
+                uint32_t dmin = 0xffffffffu;
                 int dist[NCH];
 #pragma unroll
                 for (int c = 0; c < NCH; c++) {
-                    const int sc = pk_start(td[c]);
-                    dist[c] = manhattan(pc, sc);
-                    if (need_can) can |= ballot(wprev[c] && sc == cc) != 0;
-                    if (need_idle) idle |= ballot(wprev[c] && dist[c] <= 3) != 0;
-                    if (need_near) {
-                        const int m = (int)wave_min_u32(wprev[c] ? (uint32_t)dist[c] : 1023u);
-                        dmin = m < dmin ? m : dmin;
-                    }
+                    dist[c] = manhattan(pa, stc[c]);
+                    can_a |= ballot(wv[c] && stc[c] == ca) != 0;
+                    idle_a |= ballot(wv[c] && dist[c] <= 3) != 0;
+                    const uint32_t m = wave_min_u32(wv[c] ? (uint32_t)dist[c] : 0xffffffffu);
+                    dmin = m < dmin ? m : dmin;
                 }
-                if (need_near && dmin < 1023) {
-                    // first minimum in tracker iteration order (min() over the dict)
-                    uint32_t best_o = 0xffffffffu;
+                int bc = -1;
+                if (STALE) {
+                    uint32_t omin = 0xffffffffu;
 #pragma unroll
                     for (int c = 0; c < NCH; c++) {
-                        uint64_t tie = ballot(wprev[c] && dist[c] == dmin);
-                        if (!STALE && best_o != 0xffffffffu) tie = 0;  // fresh: order == id, first tie wins
-                        while (tie) {
-                            const int jj = ffs64(tie);
-                            tie = STALE ? (tie & (tie - 1)) : 0ull;
-                            const uint32_t o = (uint32_t)rdl((int)tq[c], jj);
-                            if (o < best_o) {
-                                best_o = o;
-                                near_cell = rdl(pk_start(td[c]), jj);
-                            }
-                        }
+                        const uint32_t m = wave_min_u32(wv[c] && (uint32_t)dist[c] == dmin ? tq[c] : 0xffffffffu);
+                        omin = m < omin ? m : omin;
+                    }
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        const uint64_t b = ballot(wv[c] && (uint32_t)dist[c] == dmin && tq[c] == omin);
+                        if (b && bc < 0) bc = rdl(stc[c], ffs64(b));
+                    }
+                } else {  // fresh tracker: iteration order == id order, the first tie wins
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        const uint64_t b = ballot(wv[c] && (uint32_t)dist[c] == dmin);
+                        if (b && bc < 0) bc = rdl(stc[c], ffs64(b));
                     }
                 }
+                if (lane == a) {
+                    can = can_a;
+                    idle = idle_a;
+                    best_cell = bc;
+                }
             }
-            // 2. wasted operations
-            if (opa == 1) {
-                if (pcy != 0) s = s + C[SH_WPICK];
-                else if (ccy == 0 && !can) s = s + C[SH_WPICK];
-            } else if (opa == 2) {
-                if (pcy == 0) s = s + C[SH_WDROP];
-                else if (ccy != 0 && ppres && cc != pk_target(pdata)) s = s + C[SH_WDROP];
-            }
-            // 3. movement
-            if (mva != MV_S && !moved_a) s = s + C[SH_STUCK];
-            const int tgt = (pcy != 0 && ppres) ? pk_target(pdata) : near_cell;
-            if (tgt >= 0 && moved_a) {
-                const int db = manhattan(pc, tgt), da = manhattan(cc, tgt);
-                if (da < db) s = s + C[SH_CLOSER];
-                else if (da > db) s = s + C[SH_AWAY];
-            }
-            // 4. idle next to an available package
-            if (!moved_a && mva == MV_S && pcy == 0 && idle) s = s + C[SH_IDLE];
-            if (lane == a) s_lane = s;
         }
+        float s = 0.0f;
+        // 1. pickup / delivery
+        if (pcarry == 0 && carry != 0) s = s + C[SH_PICK];
+        else if (pcarry != 0 && carry == 0 && ppres && cell == pk_target(pdat))
+            s = s + ((t1 <= pk_dl(pdat)) ? C[SH_ONTIME] : C[SH_LATE]);
+        // 2. wasted operations
+        if (op == 1) {
+            if (pcarry != 0) s = s + C[SH_WPICK];
+            else if (carry == 0 && !can) s = s + C[SH_WPICK];
+        } else if (op == 2) {
+            if (pcarry == 0) s = s + C[SH_WDROP];
+            else if (carry != 0 && ppres && cell != pk_target(pdat)) s = s + C[SH_WDROP];
+        }
+        // 3. movement
+        const bool moved_a = pcell != cell;
+        if (mv != MV_S && !moved_a) s = s + C[SH_STUCK];
+        const int tgt = (pcarry != 0 && ppres) ? pk_target(pdat) : best_cell;
+        if (tgt >= 0 && moved_a) {
+            const int db = manhattan(pcell, tgt), da = manhattan(cell, tgt);
+            if (da < db) s = s + C[SH_CLOSER];
+            else if (da > db) s = s + C[SH_AWAY];
+        }
+        // 4. idle next to an available package
+        if (!moved_a && mv == MV_S && pcarry == 0 && idle) s = s + C[SH_IDLE];
+        s_lane = act ? s : 0.0f;
     }
     const float shaped = (float)rr + np_sum_lanes(s_lane, A);
 
@@ -476,7 +493,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
     uint32_t ctr = es.ctr;
     const bool do_rst = done && auto_reset;
-    if (STALE && !do_rst) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, carry, t1, ctr);
+    if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, carry, t1, ctr);
 
     // ---- reset on done (MAPPO/trainer.py:230-235) ----
     int t_out = t1;

@@ -16,7 +16,7 @@ import os
 import torch  # noqa: F401  (must precede loading libmdl.so, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmdl.so")
+LIB_PATH = os.environ.get("MDL_LIB_PATH") or os.path.join(HERE, "libmdl.so")  # override: profiling builds only
 
 MDL_TRACKER_FRESH = 0
 MDL_TRACKER_MAPPO_STALE = 1

@@ -109,7 +109,7 @@ __device__ inline void emit(float* dst, int n, const F& value) {
 template <class Trk>
 __device__ inline void feat_prepare(const Trk& trk, const FeatCtx& c, FeatLds& L, int cell, int carry) {
     const int lane = lane_id();
-    const int A = c.A, NS = c.NS, HW = c.HW, W = c.W, t = c.t;
+    const int A = c.A, NS = c.NS, W = c.W, t = c.t;
     if (lane < A) {
         const int r = cell_r(cell), col = cell_c(cell);
         L.rr[lane] = r;
@@ -373,110 +373,11 @@ __device__ inline void emit_critic_map(const FeatCtx& c, const FeatLds& L, float
     });
 }
 
-// generate_vector_features value of agent a, output index f (MAPPO/helper.py:68-165)
-template <class Trk>
-__device__ inline float actor_value(const Trk& trk, const FeatCtx& c, const FeatLds& L, int a, int f) {
-    const int H = c.H, W = c.W, t = c.t, T = c.T;
-    const int o_end = 6 + 5 * c.MO, p_end = o_end + 5 * c.MP;
-    const int ra = L.rr[a], ca = L.rcol[a];
-    if (f < 6) {
-        if (f == 0) return qdiv(ra, H);
-        if (f == 1) return qdiv(ca, W);
-        const int cy = L.rcarry[a];
-        if (f == 2) return cy != 0 ? 1.0f : 0.0f;
-        const int cs = L.rcslot[a];
-        if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
-        const uint64_t d = trk.data(cs);
-        const int tg = pk_target(d);
-        if (f == 3) return qdiv(cell_r(tg) - ra, H);
-        if (f == 4) return qdiv(cell_c(tg) - ca, W);
-        return dlc_over_T(pk_dl(d), t, T);
-    }
-    if (f < o_end) {
-        const int s = fdivi(f - 6, 5, 0.2f);
-        const int k = f - 6 - 5 * s;
-        if (s >= (L.cnt[a] & 0xff)) return 0.0f;
-        const int o = L.inv_o[a * 64 + s];
-        const int ro = L.rr[o], co = L.rcol[o];
-        if (k == 0) return qdiv(ro - ra, H);
-        if (k == 1) return qdiv(co - ca, W);
-        const int cy = L.rcarry[o];
-        if (k == 2) return cy != 0 ? 1.0f : 0.0f;
-        const int cs = L.rcslot[o];
-        if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
-        const int tg = pk_target(trk.data(cs));
-        if (k == 3) return qdiv(cell_r(tg) - ro, H);
-        return qdiv(cell_c(tg) - co, W);
-    }
-    if (f < p_end) {
-        const int s = fdivi(f - o_end, 5, 0.2f);
-        const int k = f - o_end - 5 * s;
-        if (s >= (L.cnt[a] >> 8) || s >= c.MPc) return 0.0f;
-        const int j = L.inv_p[a * c.MPc + s];
-        const uint64_t d = trk.data(j);
-        const int sc = pk_start(d), tg = pk_target(d);
-        switch (k) {
-            case 0: return qdiv(cell_r(sc) - ra, H);
-            case 1: return qdiv(cell_c(sc) - ca, W);
-            case 2: return qdiv(cell_r(tg) - ra, H);
-            case 3: return qdiv(cell_c(tg) - ca, W);
-            default: return dlc_over_T(pk_dl(d), t, T);
-        }
-    }
-    return T > 0 ? qdiv(t, T) : 0.0f;
-}
-
-// convert_global_state vector value at output index f (MAPPO/helper.py:199-255)
-template <class Trk>
-__device__ inline float critic_value(const Trk& trk, const FeatCtx& c, const FeatLds& L, int f) {
-    const int H = c.H, W = c.W, t = c.t, T = c.T, A = c.A, MR = c.MR;
-    const int r_end = 6 * MR, p_end = r_end + 7 * c.MPs;
-    if (f < r_end) {
-        const int i = fdivi(f, 6, 1.0f / 6.0f);
-        const int k = f - 6 * i;
-        if (i >= A) return 0.0f;
-        if (k == 0) return qdiv(L.rr[i], H);
-        if (k == 1) return qdiv(L.rcol[i], W);
-        const int cy = L.rcarry[i];
-        if (k == 2) return cy != 0 ? 1.0f : 0.0f;
-        const int cs = L.rcslot[i];
-        if (cy == 0 || cs < 0 || !trk.in_transit(cs)) return 0.0f;
-        const uint64_t d = trk.data(cs);
-        const int tg = pk_target(d);
-        if (k == 3) return qdiv(cell_r(tg), H);
-        if (k == 4) return qdiv(cell_c(tg), W);
-        return dlc_over_T(pk_dl(d), t, T);
-    }
-    if (f < p_end) {
-        const int s = fdivi(f - r_end, 7, 1.0f / 7.0f);
-        const int k = f - r_end - 7 * s;
-        if (s >= L.cnt[A + 1] || s >= c.MPsc) return 0.0f;
-        const int j = L.inv_c[s];
-        const uint64_t d = trk.data(j);
-        const bool waiting = !trk.in_transit(j);
-        const int sc = pk_start(d), tg = pk_target(d);
-        switch (k) {
-            case 0: return waiting ? qdiv(cell_r(sc), H) : 0.0f;
-            case 1: return waiting ? qdiv(cell_c(sc), W) : 0.0f;
-            case 2: return qdiv(cell_r(tg), H);
-            case 3: return qdiv(cell_c(tg), W);
-            case 4: return dlc_over_T(pk_dl(d), t, T);
-            case 5: return waiting ? 0.0f : 1.0f;
-            default: {
-                if (waiting) return -1.0f;
-                const int car = L.scar[j];
-                if (car < 0) return -1.0f;
-                return MR > 1 ? qdiv(car, MR - 1) : 0.0f;
-            }
-        }
-    }
-    return T > 0 ? qdiv(t, T) : 0.0f;
-}
-
-// Vector outputs are mostly padding.  Stage every slot that can be non-zero
-// (compact layout, one value per lane per pass, so each division runs once
-// with all lanes busy), then stream the full row: padding as literal zeros,
-// the rest read back from the staging slice.
+// Vector outputs are mostly padding.  Every tuple that can be non-zero is
+// computed by one lane into a compact staging slice (one lane per robot /
+// other-robot slot / package slot, so each value's division runs once and
+// lanes do the same kind of work), then the full row is streamed: padding as
+// literal zeros, the rest read back from the staging slice.
 __host__ __device__ inline int actor_compact_dim(int A, int MO, int MPc) {
     const int MOc = MO < A - 1 ? MO : (A - 1 > 0 ? A - 1 : 0);
     return 6 + 5 * MOc + 5 * MPc + 1;
@@ -488,6 +389,66 @@ __host__ __device__ inline int critic_compact_dim(int A, int MR, int MPsc) {
 __host__ __device__ inline int actor_group(int na, int Dc) {
     const int g = 2048 / Dc;
     return g < 1 ? 1 : (g < na ? g : na);
+}
+
+// generate_vector_features (MAPPO/helper.py:68-165): tuple `slot` of agent a
+// into out (compact layout [6 self][5*MOc others][5*MPc packages][1 time]).
+template <class Trk>
+__device__ inline void actor_tuple(const Trk& trk, const FeatCtx& c, const FeatLds& L, int a, int kind, int s,
+                                   int MOc, float* out) {
+    const int H = c.H, W = c.W, t = c.t, T = c.T;
+    const int ra = L.rr[a], ca = L.rcol[a];
+    if (kind == 0) {  // self: my_r/H, my_c/W, carrying, (tr-my_r)/H, (tc-my_c)/W, max(0,dl-t)/T ; and t/T
+        const int cy = L.rcarry[a], cs = L.rcslot[a];
+        float v3 = 0.0f, v4 = 0.0f, v5 = 0.0f;
+        if (cy != 0 && cs >= 0 && trk.in_transit(cs)) {
+            const uint64_t d = trk.data(cs);
+            const int tg = pk_target(d);
+            v3 = qdiv(cell_r(tg) - ra, H);
+            v4 = qdiv(cell_c(tg) - ca, W);
+            v5 = dlc_over_T(pk_dl(d), t, T);
+        }
+        out[0] = qdiv(ra, H);
+        out[1] = qdiv(ca, W);
+        out[2] = cy != 0 ? 1.0f : 0.0f;
+        out[3] = v3;
+        out[4] = v4;
+        out[5] = v5;
+        out[6 + 5 * MOc + 5 * c.MPc] = T > 0 ? qdiv(t, T) : 0.0f;
+    } else if (kind == 1) {  // s-th nearest other robot
+        float* o5 = out + 6 + 5 * s;
+        if (s >= (L.cnt[a] & 0xff)) {
+            o5[0] = o5[1] = o5[2] = o5[3] = o5[4] = 0.0f;
+            return;
+        }
+        const int o = L.inv_o[a * 64 + s];
+        const int ro = L.rr[o], co = L.rcol[o];
+        const int cy = L.rcarry[o], cs = L.rcslot[o];
+        float v3 = 0.0f, v4 = 0.0f;
+        if (cy != 0 && cs >= 0 && trk.in_transit(cs)) {
+            const int tg = pk_target(trk.data(cs));
+            v3 = qdiv(cell_r(tg) - ro, H);
+            v4 = qdiv(cell_c(tg) - co, W);
+        }
+        o5[0] = qdiv(ro - ra, H);
+        o5[1] = qdiv(co - ca, W);
+        o5[2] = cy != 0 ? 1.0f : 0.0f;
+        o5[3] = v3;
+        o5[4] = v4;
+    } else {  // s-th waiting package in (deadline, distance, order) order
+        float* o5 = out + 6 + 5 * MOc + 5 * s;
+        if (s >= (L.cnt[a] >> 8)) {
+            o5[0] = o5[1] = o5[2] = o5[3] = o5[4] = 0.0f;
+            return;
+        }
+        const uint64_t d = trk.data(L.inv_p[a * c.MPc + s]);
+        const int sc = pk_start(d), tg = pk_target(d);
+        o5[0] = qdiv(cell_r(sc) - ra, H);
+        o5[1] = qdiv(cell_c(sc) - ca, W);
+        o5[2] = qdiv(cell_r(tg) - ra, H);
+        o5[3] = qdiv(cell_c(tg) - ca, W);
+        o5[4] = dlc_over_T(pk_dl(d), t, T);
+    }
 }
 
 // generate_vector_features for agents [a0, a0+na): dst [na][6+5MO+5MP+1]
@@ -504,15 +465,17 @@ __device__ inline void emit_actor_vecs(const Trk& trk, const FeatCtx& c, const F
     const int o_c = 6 + 5 * MOc, p_c = o_c + 5 * c.MPc;   // compact section ends
     const int Dc = p_c + 1;
     const int o_end = 6 + 5 * c.MO, p_end = o_end + 5 * c.MP;
-    const float inv_dc = 1.0f / (float)Dc, inv_dv = 1.0f / (float)Dv;
-    const int G = actor_group(na, Dc);   // agents staged per pass
+    const int tpa = 1 + MOc + c.MPc;                        // tuples per agent
+    const float inv_tpa = 1.0f / (float)tpa, inv_dv = 1.0f / (float)Dv;
+    const int G = actor_group(na, Dc);
     for (int g0 = 0; g0 < na; g0 += G) {
         const int ng = na - g0 < G ? na - g0 : G;
-        for (int ci = lane; ci < ng * Dc; ci += WAVE) {
-            const int al = fdivi(ci, Dc, inv_dc);
-            const int cf = ci - al * Dc;
-            const int f = cf < o_c ? cf : cf < p_c ? o_end + (cf - o_c) : Dv - 1;
-            L.stage[ci] = actor_value(trk, c, L, a0 + g0 + al, f);
+        for (int ti = lane; ti < ng * tpa; ti += WAVE) {
+            const int al = fdivi(ti, tpa, inv_tpa);
+            const int k = ti - al * tpa;
+            const int kind = k == 0 ? 0 : (k <= MOc ? 1 : 2);
+            const int slot = kind == 1 ? k - 1 : k - 1 - MOc;
+            actor_tuple(trk, c, L, a0 + g0 + al, kind, slot, MOc, L.stage + al * Dc);
         }
         wave_sync();
         emit(dst + (size_t)g0 * Dv, ng * Dv, [&](int i) -> float {
@@ -530,19 +493,57 @@ __device__ inline void emit_actor_vecs(const Trk& trk, const FeatCtx& c, const F
     }
 }
 
-// convert_global_state vector: dst [6MR+7MPs+1]
+// convert_global_state vector: dst [6MR+7MPs+1] (MAPPO/helper.py:199-255)
 template <class Trk>
 __device__ inline void emit_critic_vec(const Trk& trk, const FeatCtx& c, const FeatLds& L, float* dst) {
     const int lane = lane_id();
-    const int Dg = 6 * c.MR + 7 * c.MPs + 1;
-    const int r_end = 6 * c.MR, p_end = r_end + 7 * c.MPs;
+    const int H = c.H, W = c.W, t = c.t, T = c.T, MR = c.MR;
+    const int Dg = 6 * MR + 7 * c.MPs + 1;
+    const int r_end = 6 * MR, p_end = r_end + 7 * c.MPs;
     const int nact = L.cnt[c.A + 1];
-    const int r_c = 6 * (c.A < c.MR ? c.A : c.MR);                 // robot rows present
-    const int np = nact < c.MPsc ? nact : c.MPsc;
-    const int p_c = r_c + 7 * np;                                    // package rows present
-    for (int ci = lane; ci <= p_c; ci += WAVE) {
-        const int f = ci < r_c ? ci : ci < p_c ? r_end + (ci - r_c) : Dg - 1;
-        L.stage[ci] = critic_value(trk, c, L, f);
+    const int nr = c.A < MR ? c.A : MR;                 // robot rows present
+    const int np = nact < c.MPsc ? nact : c.MPsc;       // package rows present
+    const int r_c = 6 * nr, p_c = r_c + 7 * np;
+    for (int ti = lane; ti < nr + np + 1; ti += WAVE) {
+        if (ti < nr) {  // robot row: r/H, c/W, carrying, tr/H, tc/W, max(0,dl-t)/T
+            const int cy = L.rcarry[ti], cs = L.rcslot[ti];
+            float v3 = 0.0f, v4 = 0.0f, v5 = 0.0f;
+            if (cy != 0 && cs >= 0 && trk.in_transit(cs)) {
+                const uint64_t d = trk.data(cs);
+                const int tg = pk_target(d);
+                v3 = qdiv(cell_r(tg), H);
+                v4 = qdiv(cell_c(tg), W);
+                v5 = dlc_over_T(pk_dl(d), t, T);
+            }
+            float* o = L.stage + 6 * ti;
+            o[0] = qdiv(L.rr[ti], H);
+            o[1] = qdiv(L.rcol[ti], W);
+            o[2] = cy != 0 ? 1.0f : 0.0f;
+            o[3] = v3;
+            o[4] = v4;
+            o[5] = v5;
+        } else if (ti < nr + np) {  // active package row (id order)
+            const int s = ti - nr;
+            const int j = L.inv_c[s];
+            const uint64_t d = trk.data(j);
+            const bool waiting = !trk.in_transit(j);
+            const int sc = pk_start(d), tg = pk_target(d);
+            float carrier = -1.0f;
+            if (!waiting) {
+                const int car = L.scar[j];
+                if (car >= 0) carrier = MR > 1 ? qdiv(car, MR - 1) : 0.0f;
+            }
+            float* o = L.stage + r_c + 7 * s;
+            o[0] = waiting ? qdiv(cell_r(sc), H) : 0.0f;
+            o[1] = waiting ? qdiv(cell_c(sc), W) : 0.0f;
+            o[2] = qdiv(cell_r(tg), H);
+            o[3] = qdiv(cell_c(tg), W);
+            o[4] = dlc_over_T(pk_dl(d), t, T);
+            o[5] = waiting ? 0.0f : 1.0f;
+            o[6] = carrier;
+        } else {
+            L.stage[p_c] = T > 0 ? qdiv(t, T) : 0.0f;
+        }
     }
     wave_sync();
     emit(dst, Dg, [&](int f) -> float {

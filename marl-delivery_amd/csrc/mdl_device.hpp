@@ -40,7 +40,7 @@ struct MapDesc {
 // Per-env scalars, one 16-byte record (one load / one store per step).
 struct __align__(16) EnvScalars {
     int32_t t;       // Environment.t
-    uint32_t ctr;    // tracker insertion counter (stale mode)
+    uint32_t ctr;    // reserved (0)
     double total;    // Environment.total_reward (fp64, as the reference's Python float)
 };
 
@@ -48,6 +48,12 @@ struct __align__(16) EnvScalars {
 // tracker's view of the same id (stale mode): present, in_transit, survivor
 // (inserted in an earlier episode -> its data lives in `trk`, not `pkg`).
 enum : uint32_t { PS_STATUS = 3u, PS_PRESENT = 4u, PS_TRANSIT = 8u, PS_SURVIVOR = 16u };
+
+// Tracker iteration-order keys (stale mode), all < 0x800: a survivor's key is
+// its rank among the entries present at the last reset (stored in trk.z), an
+// entry of the running episode has ORD_EPISODE + slot (spawn order == id
+// order).  Dict order == ascending key.
+constexpr uint32_t ORD_EPISODE = 0x400u;
 
 // Everything a kernel needs about the engine, passed by value.
 struct DevParams {
@@ -71,7 +77,7 @@ struct DevParams {
     EnvScalars* es;            // [E]
     uint32_t* mt;              // [E][624]
     int32_t* mt_pos;           // [E]
-    uint4* trk;                // [E][P] stale mode: (data lo, data hi, insertion seq, 0)
+    uint4* trk;                // [E][P] stale mode: (data lo, data hi, survivor order rank, 0)
     double* ep_total;          // [E] total_reward of the last finished episode
     int32_t* ep_len;           // [E]
 };
@@ -113,17 +119,17 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // min over the 64 lanes (identity 0xffffffff): DPP row_shr prefix-min inside
 // each 16-lane row, then the four row results by readlane.  Wave-uniform.
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    // row_shr 1/2/4/8 leave each row's minimum on its lane 15; row_bcast:15
+    // and row_bcast:31 carry it across rows, so lane 63 holds the wave's.
     const int id = (int)0xffffffff;
     uint32_t t;
     t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xf, 0xf, false); v = t < v ? t : v;  // row_shr:1
     t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xf, 0xf, false); v = t < v ? t : v;  // row_shr:2
     t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xf, 0xf, false); v = t < v ? t : v;  // row_shr:4
     t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xf, 0xf, false); v = t < v ? t : v;  // row_shr:8
-    uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
-    uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, 31); m = x < m ? x : m;
-    x = (uint32_t)__builtin_amdgcn_readlane((int)v, 47); m = x < m ? x : m;
-    x = (uint32_t)__builtin_amdgcn_readlane((int)v, 63); m = x < m ? x : m;
-    return m;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x142, 0xa, 0xf, false); v = t < v ? t : v;  // row_bcast:15
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x143, 0xc, 0xf, false); v = t < v ? t : v;  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // Correctly rounded int/int division in float32.  For |a|,|b| < 2^24 this
@@ -321,13 +327,13 @@ struct TrkFresh {  // == env truth: ids in spawn (= id) order
 };
 
 // Explicit per-id slots, never cleared on auto-reset.  Iteration order:
-// survivors of earlier episodes by insertion seq, then this episode's
+// survivors of earlier episodes by their rank, then this episode's
 // insertions, which happen in id order (spawn order == id order).
 struct TrkStale {
     static constexpr bool kIdIndexed = true;
     const uint8_t* ps;
     const uint64_t* td;   // survivor ? trk data : pkg
-    const uint32_t* tq;   // survivor ? seq : 0x80000000 + id
+    const uint32_t* tq;   // survivor ? rank : ORD_EPISODE + slot
     int n;
     __device__ int count() const { return n; }
     __device__ bool present(int j) const { return (ps[j] & PS_PRESENT) != 0; }

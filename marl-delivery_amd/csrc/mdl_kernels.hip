@@ -82,24 +82,20 @@ __device__ inline int do_reset(const DevParams& p, int e, const MapDesc& md, Res
 
 // Tracker update on lane-resident package state (MAPPO/trainer.py:95-130):
 // insert ids spawned at t that are absent (in id order), then carried ->
-// in_transit, in_transit & not carried -> delete.
+// in_transit, in_transit & not carried -> delete.  An inserted entry's order
+// key is implicit (ORD_EPISODE + slot) until the next reset.
 template <int NCH>
-__device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[NCH], uint32_t (&tq)[NCH],
-                                           bool (&dirty)[NCH], const uint64_t (&pk)[NCH], int P, int A, int carry,
-                                           int t, uint32_t& ctr) {
+__device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[NCH], bool (&dirty)[NCH],
+                                           const uint64_t (&pk)[NCH], int P, int A, int carry, int t) {
     const int lane = lane_id();
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
-        const bool ins = j < P && pk_st(pk[c]) == t && !(ps[c] & PS_PRESENT);
-        const uint64_t b = ballot(ins);
-        if (ins) {
+        if (j < P && pk_st(pk[c]) == t && !(ps[c] & PS_PRESENT)) {
             ps[c] = (ps[c] & PS_STATUS) | PS_PRESENT;
             td[c] = pk[c];
-            tq[c] = ctr + (uint32_t)popc64(b & lanemask_lt());  // insertion seq (stored)
             dirty[c] = true;
         }
-        ctr += (uint32_t)popc64(b);
     }
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
@@ -109,6 +105,38 @@ __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[N
         if (ps[c] & PS_PRESENT) {
             if (carried) ps[c] |= PS_TRANSIT;
             else if (ps[c] & PS_TRANSIT) ps[c] &= PS_STATUS;
+        }
+    }
+}
+
+// Reset with a persistent tracker: every present entry becomes a survivor
+// whose key is its rank in the current dict order (keys `tq`: survivor rank
+// or ORD_EPISODE + slot, distinct), so keys stay below ORD_EPISODE forever.
+// Returns the new ranks in `tq`; `renum` marks the entries to store.
+template <int NCH>
+__device__ inline void survivors_at_reset(uint32_t (&ps)[NCH], uint32_t (&tq)[NCH], bool (&renum)[NCH], int P) {
+    const int lane = lane_id();
+    uint32_t rk[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) rk[c] = 0;
+#pragma unroll
+    for (int c2 = 0; c2 < NCH; c2++) {
+        uint64_t m = ballot(c2 * WAVE + lane < P && (ps[c2] & PS_PRESENT));
+        while (m) {
+            const uint32_t ki = (uint32_t)rdl((int)tq[c2], ffs64(m));
+            m &= m - 1;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) rk[c] += ki < tq[c] ? 1u : 0u;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        renum[c] = c * WAVE + lane < P && (ps[c] & PS_PRESENT);
+        if (renum[c]) {
+            tq[c] = rk[c];
+            ps[c] |= PS_SURVIVOR;
+        } else {
+            ps[c] &= PS_STATUS;
         }
     }
 }
@@ -165,28 +193,28 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restric
     const int A = p.A, P = p.P;
     ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
     const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
-    uint32_t ps[NCH];
+    uint32_t ps[NCH], tq[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
         ps[c] = j < P ? p.pstate[(size_t)e * P + j] : 0u;
+        tq[c] = ORD_EPISODE + (uint32_t)j;
+        if (p.stale && (ps[c] & PS_SURVIVOR)) tq[c] = p.trk[(size_t)e * P + j].z;
     }
     const int cell = do_reset(p, e, md, L, false);
-    uint32_t ctr = p.es[e].ctr;
     uint64_t pk[NCH], td[NCH];
-    uint32_t tq[NCH];
-    bool dirty[NCH];
+    bool dirty[NCH], renum[NCH];
+    if (p.stale) survivors_at_reset<NCH>(ps, tq, renum, P);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
         pk[c] = j < P ? L.pk[j] : 0;
-        const uint32_t trk = (ps[c] & PS_PRESENT) ? ((ps[c] & ~PS_STATUS) | PS_SURVIVOR) : 0u;
-        ps[c] = (j < P ? L.pst[j] : 0u) | (p.stale ? trk : 0u);
+        ps[c] = (j < P ? L.pst[j] : 0u) | (p.stale ? (ps[c] & ~PS_STATUS) : 0u);
+        if (!p.stale) renum[c] = false;
         td[c] = pk[c];
-        tq[c] = 0;
         dirty[c] = false;
     }
-    if (p.stale) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, 0, 0, ctr);
+    if (p.stale) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, 0, 0);
     if (lane < A)
         p.rob[(size_t)e * A + lane] = rob_pack(cell, 0, p.movevalid[md.grid_off + cell_r(cell) * md.W + cell_c(cell)]);
 #pragma unroll
@@ -196,13 +224,14 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restric
             const size_t g = (size_t)e * P + j;
             p.pkg[g] = pk[c];
             p.pstate[g] = (uint8_t)ps[c];
-            if (dirty[c]) p.trk[g] = make_uint4((uint32_t)td[c], (uint32_t)(td[c] >> 32), tq[c], 0u);
+            if (dirty[c]) p.trk[g] = make_uint4((uint32_t)td[c], (uint32_t)(td[c] >> 32), 0u, 0u);
+            else if (renum[c]) reinterpret_cast<uint32_t*>(p.trk + g)[2] = tq[c];
         }
     }
     if (lane == 0) {
         EnvScalars s;
         s.t = 0;
-        s.ctr = ctr;
+        s.ctr = 0;
         s.total = 0.0;
         p.es[e] = s;
     }
@@ -269,13 +298,13 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     int cell = rob_cell(rv), carry = rob_carry(rv);
     uint32_t vmask = rob_valid(rv);
     const int t0 = es.t;
-    // tracker_prev view: data / iteration order per slot
+    // tracker_prev view: data / iteration order key (< 0x800) per slot
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
-        const int id = c * WAVE + lane + 1;
+        const int j = c * WAVE + lane;
         if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
             td[c] = pk[c];
-            tq[c] = STALE ? 0x80000000u + (uint32_t)id : (uint32_t)id;
+            tq[c] = STALE ? ORD_EPISODE + (uint32_t)j : (uint32_t)j;
         }
     }
 
@@ -378,9 +407,11 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     const bool done = (t1 == p.T) || (ndel == P);
 
     // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
-    // Agents on lanes (VALU work); one wave-uniform pass over the waiting
-    // packages of tracker_prev (st <= t_prev) serves every agent's
-    // can-pick-up / idle-nearby / nearest-target query.
+    // Agents on lanes.  Each agent that needs the nearest waiting package of
+    // tracker_prev (st <= t_prev) gets it from one DPP minimum over the package
+    // lanes of (distance << 11 | order key); idle-nearby is that distance <= 3.
+    // The reference's if-chains become selects: adding 0.0f is exact here
+    // (s starts at +0 and never becomes -0).
     float s_lane = 0.0f;
     if (!(MDL_ABLATE & 1)) {
         const float* C = p.shaping;
@@ -402,102 +433,96 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         const bool ppres = act && pcarry != 0 && pcarry <= P &&
                            (STALE ? (pf & PS_PRESENT) != 0
                                   : ((pf & PS_STATUS) == ST_WAITING || (pf & PS_STATUS) == ST_IN_TRANSIT));
-        // Per agent (uniform loop): distances on the package lanes, answers
-        // by ballot (can pick up here / idle next to a package) and DPP
-        // minima (nearest waiting package, ties by tracker iteration order);
-        // results land on the agent's lane.
+        const bool moved_a = pcell != cell;
+        const bool need_near = act && moved_a && !(pcarry != 0 && ppres);
+        const bool need_idle = act && !moved_a && mv == MV_S && pcarry == 0;
+        const bool need_can = act && op == 1 && pcarry == 0 && carry == 0;
         bool wv[NCH];
         int stc[NCH];
+        uint64_t anyw = 0;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const uint32_t f = ps0[c];
             const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
             wv[c] = waiting && pk_st(td[c]) <= t0;
             stc[c] = pk_start(td[c]);
+            anyw |= ballot(wv[c]);
         }
-        uint64_t anyw = 0;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) anyw |= ballot(wv[c]);
-        bool can = false, idle = false;
+        // per-agent answers: bit masks in SGPRs, the nearest start cell written
+        // into the agent's lane
+        uint64_t idle_m = 0, can_m = 0;
         int best_cell = -1;
         if (anyw) {
-            for (int a = 0; a < A; a++) {
-                const int pa = rdl(pcell, a), ca = rdl(cell, a);
-                bool can_a = false, idle_a = false;
-                uint32_t dmin = 0xffffffffu;
-                int dist[NCH];
+            for (uint64_t q = ballot(need_near || need_idle); q; q &= q - 1) {
+                const int a = ffs64(q);
+                const int pa = rdl(pcell, a);
+                uint32_t key[NCH];
+                uint32_t kmin = 0xffffffffu;
 #pragma unroll
                 for (int c = 0; c < NCH; c++) {
-                    dist[c] = manhattan(pa, stc[c]);
-                    can_a |= ballot(wv[c] && stc[c] == ca) != 0;
-                    idle_a |= ballot(wv[c] && dist[c] <= 3) != 0;
-                    const uint32_t m = wave_min_u32(wv[c] ? (uint32_t)dist[c] : 0xffffffffu);
-                    dmin = m < dmin ? m : dmin;
+                    key[c] = wv[c] ? ((uint32_t)manhattan(pa, stc[c]) << 11) | tq[c] : 0xffffffffu;
+                    const uint32_t m = wave_min_u32(key[c]);
+                    kmin = m < kmin ? m : kmin;
                 }
                 int bc = -1;
-                if (STALE) {
-                    uint32_t omin = 0xffffffffu;
 #pragma unroll
-                    for (int c = 0; c < NCH; c++) {
-                        const uint32_t m = wave_min_u32(wv[c] && (uint32_t)dist[c] == dmin ? tq[c] : 0xffffffffu);
-                        omin = m < omin ? m : omin;
-                    }
-#pragma unroll
-                    for (int c = 0; c < NCH; c++) {
-                        const uint64_t b = ballot(wv[c] && (uint32_t)dist[c] == dmin && tq[c] == omin);
-                        if (b && bc < 0) bc = rdl(stc[c], ffs64(b));
-                    }
-                } else {  // fresh tracker: iteration order == id order, the first tie wins
-#pragma unroll
-                    for (int c = 0; c < NCH; c++) {
-                        const uint64_t b = ballot(wv[c] && (uint32_t)dist[c] == dmin);
-                        if (b && bc < 0) bc = rdl(stc[c], ffs64(b));
-                    }
+                for (int c = 0; c < NCH; c++) {
+                    const uint64_t b = ballot(key[c] == kmin);
+                    const int v = rdl(stc[c], ffs64(b) & 63);
+                    bc = b ? v : bc;
                 }
-                if (lane == a) {
-                    can = can_a;
-                    idle = idle_a;
-                    best_cell = bc;
-                }
+                idle_m |= (uint64_t)((kmin >> 11) <= 3u) << a;
+                best_cell = lane == a ? bc : best_cell;
+            }
+            for (uint64_t q = ballot(need_can); q; q &= q - 1) {
+                const int a = ffs64(q);
+                const int ca = rdl(cell, a);
+                uint64_t h = 0;
+#pragma unroll
+                for (int c = 0; c < NCH; c++) h |= ballot(wv[c] && stc[c] == ca);
+                can_m |= (uint64_t)(h != 0) << a;
             }
         }
+        const bool idle = (idle_m >> lane) & 1ull, can = (can_m >> lane) & 1ull;
+        // the constants, pinned in SGPRs so the selects below stay branch-free
+        float cs[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            cs[k] = C[k];
+            asm volatile("" : "+s"(cs[k]));
+        }
+        const int ptg = pk_target(pdat);
         float s = 0.0f;
         // 1. pickup / delivery
-        if (pcarry == 0 && carry != 0) s = s + C[SH_PICK];
-        else if (pcarry != 0 && carry == 0 && ppres && cell == pk_target(pdat))
-            s = s + ((t1 <= pk_dl(pdat)) ? C[SH_ONTIME] : C[SH_LATE]);
+        const bool pick = pcarry == 0 && carry != 0;
+        const bool deliv = pcarry != 0 && carry == 0 && ppres && cell == ptg;
+        s = s + (pick ? cs[SH_PICK] : deliv ? ((t1 <= pk_dl(pdat)) ? cs[SH_ONTIME] : cs[SH_LATE]) : 0.0f);
         // 2. wasted operations
-        if (op == 1) {
-            if (pcarry != 0) s = s + C[SH_WPICK];
-            else if (carry == 0 && !can) s = s + C[SH_WPICK];
-        } else if (op == 2) {
-            if (pcarry == 0) s = s + C[SH_WDROP];
-            else if (carry != 0 && ppres && cell != pk_target(pdat)) s = s + C[SH_WDROP];
-        }
+        const bool wpick = op == 1 && (pcarry != 0 || (carry == 0 && !can));
+        const bool wdrop = op == 2 && (pcarry == 0 || (carry != 0 && ppres && cell != ptg));
+        s = s + (wpick ? cs[SH_WPICK] : wdrop ? cs[SH_WDROP] : 0.0f);
         // 3. movement
-        const bool moved_a = pcell != cell;
-        if (mv != MV_S && !moved_a) s = s + C[SH_STUCK];
-        const int tgt = (pcarry != 0 && ppres) ? pk_target(pdat) : best_cell;
-        if (tgt >= 0 && moved_a) {
-            const int db = manhattan(pcell, tgt), da = manhattan(cell, tgt);
-            if (da < db) s = s + C[SH_CLOSER];
-            else if (da > db) s = s + C[SH_AWAY];
-        }
+        s = s + ((mv != MV_S && !moved_a) ? cs[SH_STUCK] : 0.0f);
+        const int tgt = (pcarry != 0 && ppres) ? ptg : best_cell;
+        const int db = manhattan(pcell, tgt), da = manhattan(cell, tgt);
+        s = s + ((tgt >= 0 && moved_a) ? (da < db ? cs[SH_CLOSER] : da > db ? cs[SH_AWAY] : 0.0f) : 0.0f);
         // 4. idle next to an available package
-        if (!moved_a && mv == MV_S && pcarry == 0 && idle) s = s + C[SH_IDLE];
+        s = s + ((!moved_a && mv == MV_S && pcarry == 0 && idle) ? cs[SH_IDLE] : 0.0f);
         s_lane = act ? s : 0.0f;
     }
     const float shaped = (float)rr + np_sum_lanes(s_lane, A);
 
     // ---- tracker update with the new state; a done env that resets here skips
     // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
-    uint32_t ctr = es.ctr;
     const bool do_rst = done && auto_reset;
-    if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, carry, t1, ctr);
+    if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, carry, t1);
 
     // ---- reset on done (MAPPO/trainer.py:230-235) ----
     int t_out = t1;
     double total_out = total;
+    bool renum[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) renum[c] = false;
     if (do_rst) {
         ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
         const int nc = do_reset(p, e, md, L, false);
@@ -506,14 +531,14 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             carry = 0;
             vmask = p.movevalid[md.grid_off + cell_r(cell) * md.W + cell_c(cell)];
         }
+        if (STALE) survivors_at_reset<NCH>(ps, tq, renum, P);
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const int j = c * WAVE + lane;
             pk[c] = j < P ? L.pk[j] : 0;
-            const uint32_t trk = (ps[c] & PS_PRESENT) ? ((ps[c] & ~PS_STATUS) | PS_SURVIVOR) : 0u;
-            ps[c] = (j < P ? L.pst[j] : 0u) | (STALE ? trk : 0u);
+            ps[c] = (j < P ? L.pst[j] : 0u) | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
         }
-        if (STALE) tracker_update_regs<NCH>(ps, td, tq, dirty, pk, P, A, 0, 0, ctr);
+        if (STALE) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, 0, 0);
         t_out = 0;
         total_out = 0.0;
     }
@@ -527,13 +552,14 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             const size_t g = (size_t)e * P + j;
             if (ps[c] != ps0[c]) p.pstate[g] = (uint8_t)ps[c];
             if (do_rst) p.pkg[g] = pk[c];
-            if (STALE && dirty[c]) p.trk[g] = make_uint4((uint32_t)td[c], (uint32_t)(td[c] >> 32), tq[c], 0u);
+            if (STALE && (dirty[c] || renum[c]))
+                p.trk[g] = make_uint4((uint32_t)td[c], (uint32_t)(td[c] >> 32), renum[c] ? tq[c] : 0u, 0u);
         }
     }
     if (lane == 0) {
         EnvScalars s;
         s.t = t_out;
-        s.ctr = ctr;
+        s.ctr = 0;
         s.total = total_out;
         p.es[e] = s;
         if (done) {
@@ -604,7 +630,7 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
         S.ps[j] = (uint8_t)f;
         if (STALE) {
             uint64_t td = d;
-            uint32_t tq = 0x80000000u + (uint32_t)(j + 1);
+            uint32_t tq = ORD_EPISODE + (uint32_t)j;
             if (f & PS_SURVIVOR) {
                 const uint4 v = p.trk[g];
                 td = (uint64_t)v.x | ((uint64_t)v.y << 32);
@@ -788,7 +814,7 @@ __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict
         if (p.stale) {
             present = (f & PS_PRESENT) ? 1 : 0;
             intr = (f & PS_TRANSIT) ? 1 : 0;
-            order = 0x80000000u + (uint32_t)(j + 1);
+            order = ORD_EPISODE + (uint32_t)j;
             if (f & PS_SURVIVOR) {
                 const uint4 v = p.trk[g];
                 td = (uint64_t)v.x | ((uint64_t)v.y << 32);
@@ -801,8 +827,7 @@ __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict
         }
         if (trk) {
             int32_t* o = trk + g * 4;
-            // order as a signed int32 that sorts like the unsigned key
-            o[0] = present; o[1] = intr; o[2] = (int32_t)(order ^ 0x80000000u); o[3] = (f & PS_SURVIVOR) ? 1 : 0;
+            o[0] = present; o[1] = intr; o[2] = (int32_t)order; o[3] = (f & PS_SURVIVOR) ? 1 : 0;
         }
         if (trk_data) {
             int32_t* o = trk_data + g * 6;

@@ -94,6 +94,9 @@ __host__ __device__ __forceinline__ uint32_t rob_valid(uint32_t w) { return (w >
 
 // ---------------------------------------------------------------- wave utils
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+// wave index in the workgroup as a wave-uniform (SGPR) value, so per-env
+// addressing and the map descriptor lookup are scalar
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -102,6 +105,16 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// Global (address space 1) pointer qualifier: keeps loads through pinned
+// pointer copies global_load / s_load instead of flat.
+#define GLOBAL __attribute__((address_space(1)))
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // POD 16-byte vector
+
+// Materialise a wave-uniform value in SGPRs at this point (the compiler may
+// neither sink its load below nor recompute it after).
+template <class T>
+__device__ __forceinline__ void pin(T& v) { asm volatile("" : "+s"(v)); }
 
 __device__ __forceinline__ int rdl(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
 __device__ __forceinline__ float rdlf(float v, int j) {

@@ -28,6 +28,19 @@
 
 namespace mdl {
 
+// Diagnostic build only (scripts/exp/stamps.sh): s_memtime per section of k_step.
+#ifdef MDL_STAMPS
+__device__ uint64_t g_stamps[65536 * 16];
+#define STAMP(k)                                                                          \
+    do {                                                                                  \
+        if (lane == 0) g_stamps[(size_t)w * 16 + (k)] = __builtin_amdgcn_s_memtime();     \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+
 // floats of the vector staging slice: max(actor rows of `na` agents, critic row)
 __host__ __device__ inline int stage_floats(int A, int na, int MO, int MPc, int MR, int MPsc) {
     const int dc = actor_compact_dim(A, MO, MPc);
@@ -145,7 +158,7 @@ __device__ inline void survivors_at_reset(uint32_t (&ps)[NCH], uint32_t (&tq)[NC
 __global__ __launch_bounds__(256) void k_seed(DevParams p, const uint32_t* __restrict__ seeds, int wpb,
                                               int lds_stride) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int lane = lane_id();
     const int e = blockIdx.x * wpb + wave;
     if (wave >= wpb || e >= p.E) return;
@@ -185,7 +198,7 @@ template <int NCH>
 __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restrict__ env_ids, int n, int wpb,
                                                int lds_stride) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int lane = lane_id();
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
@@ -238,7 +251,7 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restric
 }
 
 __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* __restrict__ env_ids, int n) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int w = blockIdx.x * 4 + wave;
     if (w >= n) return;
     const int e = env_ids ? env_ids[w] : w;
@@ -256,20 +269,45 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
                                               double* __restrict__ r_out, float* __restrict__ sh_out,
                                               uint8_t* __restrict__ done_out, int wpb, int lds_stride) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = threadIdx.x >> 6;
-    const int lane = lane_id();
-    const int w = blockIdx.x * wpb + wave;
-    if (wave >= wpb || w >= n) return;
-    const int e = env_ids ? env_ids[w] : w;
-    const int A = p.A, P = p.P;
-    const int mi = p.env_map ? p.env_map[e] : 0;
-    const MapDesc md = p.maps[mi];
+    // The kernel arguments the loads below need, fetched in one scalar batch
+    // and pinned there (left alone, the compiler sinks each to its first use
+    // and the wave pays one dependent scalar-cache miss per argument line).
+    // The batch touches every kernarg line the step reads, so the arguments
+    // read later (constants, output pointers) hit the scalar cache.
+    int A = p.A, P = p.P, T = p.T;
+    GLOBAL const uint8_t* env_map = (GLOBAL const uint8_t*)p.env_map;
+    GLOBAL const uint8_t* mvalid = (GLOBAL const uint8_t*)p.movevalid;
+    GLOBAL uint32_t* robp = (GLOBAL uint32_t*)p.rob;
+    GLOBAL uint64_t* pkgp = (GLOBAL uint64_t*)p.pkg;
+    GLOBAL uint8_t* pstp = (GLOBAL uint8_t*)p.pstate;
+    GLOBAL u32x4* esp = (GLOBAL u32x4*)p.es;   // EnvScalars {t, ctr, total lo, total hi}
+    GLOBAL u32x4* trkp = (GLOBAL u32x4*)p.trk;
+    int mW = p.maps[0].W, mgoff = p.maps[0].grid_off;
+    GLOBAL const uint8_t* actp = (GLOBAL const uint8_t*)actions;
+    GLOBAL const int* idsp = (GLOBAL const int*)env_ids;
+    int fmt_ = fmt, n_ = n, wpb_ = wpb;
+    float c_touch = p.shaping[8];
+    double* rop = r_out;
+    pin(A); pin(P); pin(T); pin(env_map); pin(mvalid); pin(robp); pin(pkgp); pin(pstp); pin(esp); pin(trkp);
+    pin(mW); pin(mgoff); pin(actp); pin(idsp); pin(fmt_); pin(n_); pin(wpb_); pin(c_touch); pin(rop);
 
+    const int wave = wave_id();
+    const int lane = lane_id();
+    const int w = blockIdx.x * wpb_ + wave;
+    if (wave >= wpb_ || w >= n_) return;
+    const int e = idsp ? uni(idsp[w]) : w;
+    int mi = 0;
+    if (env_map) {
+        mi = uni(env_map[e]);
+        mW = p.maps[mi].W;
+        mgoff = p.maps[mi].grid_off;
+    }
+
+    STAMP(0);
     // ---- loads: one round trip, everything independent ----
-    const EnvScalars es = p.es[e];
     const bool act = lane < A;
-    const uint32_t rv = act ? p.rob[(size_t)e * A + lane] : 0u;
-    const int araw = act ? (int)actions[(size_t)w * A + lane] : 0;
+    const uint32_t rv = act ? robp[(size_t)e * A + lane] : 0u;
+    const int araw = act ? (int)actp[(size_t)w * A + lane] : 0;
     uint64_t pk[NCH], td[NCH];
     uint32_t ps[NCH], ps0[NCH], tq[NCH];
     bool dirty[NCH];
@@ -283,21 +321,23 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         dirty[c] = false;
         if (j < P) {
             const size_t g = (size_t)e * P + j;
-            pk[c] = p.pkg[g];
-            ps[c] = p.pstate[g];
+            pk[c] = pkgp[g];
+            ps[c] = pstp[g];
             if (STALE) {
-                const uint4 v = p.trk[g];
+                const u32x4 v = trkp[g];
                 td[c] = (uint64_t)v.x | ((uint64_t)v.y << 32);
                 tq[c] = v.z;
             }
         }
         ps0[c] = ps[c];
     }
+    const u32x4 esv = esp[e];
+    __builtin_amdgcn_sched_barrier(0);  // every load above is issued before any use
     int mv = MV_S, op = 0;
-    if (act) decode_action(araw, fmt, mv, op);
+    if (act) decode_action(araw, fmt_, mv, op);
     int cell = rob_cell(rv), carry = rob_carry(rv);
     uint32_t vmask = rob_valid(rv);
-    const int t0 = es.t;
+    const int t0 = (int)esv.x;
     // tracker_prev view: data / iteration order key (< 0x800) per slot
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
@@ -308,6 +348,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         }
     }
 
+    STAMP(1);
     // ---- movement (env.py:188-257) ----
     // moved = least fixed point of
     //   moved[i] = mover[i] & winner(prop[i]) == i & (occ(prop[i]) none | moved[occ])
@@ -315,33 +356,37 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     // loop, checked against the oracle's literal restatement.
     const int pcell = cell, pcarry = carry;
     int prop = cell;
-    if (act && ((vmask >> mv) & 1u))   // bits 1..4 only: S / other moves never move
-        prop = cell + (mv == MV_L ? -256 : mv == MV_R ? 256 : mv == MV_U ? -1 : 1);
+    if (act && ((vmask >> mv) & 1u)) {  // bits 1..4 only: S / other moves never move
+        const int m = mv <= MV_R ? 256 : 1;  // L -256, R +256, U -1, D +1
+        prop = cell + ((mv & 1) ? -m : m);
+    }
     const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
     const uint64_t movers = ballot(mover);
     uint64_t moved = 0;
     if (movers) {
-        bool win = true;
-        int occ = -1;
-        for (int j = 0; j < A; j++) {
-            const int pj = rdl(cell, j), qj = rdl(prop, j);
-            if (j < lane && ((movers >> j) & 1ull) && qj == prop) win = false;
-            if (pj == prop) occ = j;
+        // blocked: a lower-index mover proposes the same cell; occ: the robot
+        // now standing on the proposed cell (robots stand on distinct cells)
+        int blocked = 0, occ = -1;
+        for (uint64_t m = movers; m; m &= m - 1) {
+            const int j = ffs64(m);
+            blocked |= (int)(j < lane) & (int)(rdl(prop, j) == prop);
         }
-        const bool base = mover && win;
+        for (int j = 0; j < A; j++) occ = rdl(cell, j) == prop ? j : occ;
+        const bool base = mover && !blocked;
         for (int it = 0; it <= A; it++) {
-            const bool m = base && (occ < 0 || ((moved >> occ) & 1ull));
+            const bool m = base && (occ < 0 || ((moved >> (occ & 63)) & 1ull));
             const uint64_t nm = ballot(m);
             if (nm == moved) break;
             moved = nm;
         }
         if ((moved >> lane) & 1ull) {
             cell = prop;
-            vmask = p.movevalid[md.grid_off + cell_r(cell) * md.W + cell_c(cell)];  // consumed at write-back
+            vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];  // consumed at write-back
         }
     }
     const int n_cost = popc64(moved);
 
+    STAMP(2);
     // ---- package actions (env.py:259-292); robots sit on distinct cells, so
     // pick-ups and drops of different robots never interact ----
     uint64_t pickers = ballot(!(MDL_ABLATE & 8) && act && op == 1 && carry == 0);
@@ -394,8 +439,9 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         rr += ((omask >> i) & 1ull) ? p.delivery_reward : p.delay_reward;
     }
     const int t1 = t0 + 1;
-    const double total = es.total + rr;
+    const double total = __hiloint2double((int)esv.w, (int)esv.z) + rr;
 
+    STAMP(3);
     // ---- terminate (env.py:308-316) + spawn (get_state env.py:133-137) ----
     int ndel = 0;
 #pragma unroll
@@ -404,8 +450,9 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         ndel += popc64(ballot((ps[c] & PS_STATUS) == ST_DELIVERED));
         if (j < P && pk_st(pk[c]) == t1) ps[c] = (ps[c] & ~PS_STATUS) | ST_WAITING;
     }
-    const bool done = (t1 == p.T) || (ndel == P);
+    const bool done = (t1 == T) || (ndel == P);
 
+    STAMP(4);
     // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
     // Agents on lanes.  Each agent that needs the nearest waiting package of
     // tracker_prev (st <= t_prev) gets it from one DPP minimum over the package
@@ -414,7 +461,6 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     // (s starts at +0 and never becomes -0).
     float s_lane = 0.0f;
     if (!(MDL_ABLATE & 1)) {
-        const float* C = p.shaping;
         // tracker_prev entry of each agent's previously carried id (ds_bpermute gather)
         const int pj = pcarry - 1;
         uint32_t pf = 0;
@@ -488,8 +534,8 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         float cs[9];
 #pragma unroll
         for (int k = 0; k < 9; k++) {
-            cs[k] = C[k];
-            asm volatile("" : "+s"(cs[k]));
+            cs[k] = p.shaping[k];
+            pin(cs[k]);
         }
         const int ptg = pk_target(pdat);
         float s = 0.0f;
@@ -512,6 +558,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     }
     const float shaped = (float)rr + np_sum_lanes(s_lane, A);
 
+    STAMP(5);
     // ---- tracker update with the new state; a done env that resets here skips
     // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
     const bool do_rst = done && auto_reset;
@@ -525,11 +572,12 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     for (int c = 0; c < NCH; c++) renum[c] = false;
     if (do_rst) {
         ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
+        const MapDesc md = p.maps[mi];
         const int nc = do_reset(p, e, md, L, false);
         if (act) {
             cell = nc;
             carry = 0;
-            vmask = p.movevalid[md.grid_off + cell_r(cell) * md.W + cell_c(cell)];
+            vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];
         }
         if (STALE) survivors_at_reset<NCH>(ps, tq, renum, P);
 #pragma unroll
@@ -543,33 +591,31 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         total_out = 0.0;
     }
 
+    STAMP(6);
     // ---- write back only what changed ----
-    if (act) p.rob[(size_t)e * A + lane] = rob_pack(cell, carry, vmask);
+    if (act) robp[(size_t)e * A + lane] = rob_pack(cell, carry, vmask);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
         if (j < P) {
             const size_t g = (size_t)e * P + j;
-            if (ps[c] != ps0[c]) p.pstate[g] = (uint8_t)ps[c];
-            if (do_rst) p.pkg[g] = pk[c];
+            if (ps[c] != ps0[c]) pstp[g] = (uint8_t)ps[c];
+            if (do_rst) pkgp[g] = pk[c];
             if (STALE && (dirty[c] || renum[c]))
-                p.trk[g] = make_uint4((uint32_t)td[c], (uint32_t)(td[c] >> 32), renum[c] ? tq[c] : 0u, 0u);
+                trkp[g] = u32x4{(uint32_t)td[c], (uint32_t)(td[c] >> 32), renum[c] ? tq[c] : 0u, 0u};
         }
     }
     if (lane == 0) {
-        EnvScalars s;
-        s.t = t_out;
-        s.ctr = 0;
-        s.total = total_out;
-        p.es[e] = s;
+        esp[e] = u32x4{(uint32_t)t_out, 0u, (uint32_t)__double2loint(total_out), (uint32_t)__double2hiint(total_out)};
         if (done) {
             p.ep_total[e] = total;
             p.ep_len[e] = t1;
         }
-        if (r_out) r_out[w] = rr;
+        if (rop) rop[w] = rr;
         if (sh_out) sh_out[w] = shaped;
         if (done_out) done_out[w] = done ? 1 : 0;
     }
+    STAMP(7);
 }
 
 // ------------------------------------------------------------- observations
@@ -590,7 +636,7 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
                                              float* __restrict__ avec, float* __restrict__ cmap,
                                              float* __restrict__ cvec, int wpb, int lds_stride) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int lane = lane_id();
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
@@ -721,7 +767,7 @@ __global__ __launch_bounds__(256) void k_views_features(DevParams p, const int32
                                                         float* __restrict__ gmap, float* __restrict__ gvec, int wpb,
                                                         int lds_stride, int HW) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
     unsigned char* base = smem + (size_t)wave * lds_stride;
@@ -759,7 +805,7 @@ __global__ __launch_bounds__(256) void k_views_shaped(DevParams p, const int32_t
                                                       const double* __restrict__ g, int n, ShapingConsts C,
                                                       float* __restrict__ out, int wpb, int lds_stride, int NSmax) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int lane = lane_id();
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
@@ -785,7 +831,7 @@ __global__ __launch_bounds__(256) void k_views_shaped(DevParams p, const int32_t
 __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict__ robots, int32_t* __restrict__ pkgs,
                                                 int32_t* __restrict__ tt, double* __restrict__ total,
                                                 int32_t* __restrict__ trk, int32_t* __restrict__ trk_data) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int lane = lane_id();
     const int e = blockIdx.x * 4 + wave;
     if (e >= p.E) return;
@@ -952,3 +998,9 @@ size_t views_lds(int NSmax, int HW, int MO, int MPc, int MR, int MPsc) {
 size_t views_shaped_lds(int NSmax) { return view_pre_bytes(NSmax); }
 
 }  // namespace mdl
+
+#ifdef MDL_STAMPS
+extern "C" int mdl_debug_stamps(void* dst, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(mdl::g_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -1,0 +1,40 @@
+"""Per-section cycle costs of k_step from the MDL_STAMPS diagnostic build (profiling only).
+
+Run with MDL_LIB_PATH=marl-delivery_amd/build/stamps/libmdl.so."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "marl-delivery_amd"))
+import marl_gpu  # noqa: E402
+from marl_gpu import _lib  # noqa: E402
+from marl_gpu.maps import grid_array, load_map, map_path  # noqa: E402
+
+names = ["loads", "move", "pkgs", "term", "shaping", "tracker", "write"]
+res = {}
+for E in [int(x) for x in (sys.argv[1:] or ["1024", "4096"])]:
+    env = marl_gpu.BatchedEnv(grid_array(load_map(map_path("map1.txt"))), E, 5, 50, 500, seed=42, tracker="mappo")
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    acts = torch.randint(0, 15, (300, E, 5), dtype=torch.uint8, device="cuda", generator=g)
+    for k in range(300):
+        env.step(acts[k])
+    torch.cuda.synchronize()
+    buf = np.zeros((65536, 16), np.uint64)
+    assert _lib.lib().mdl_debug_stamps(C.c_void_p(buf.ctypes.data), C.c_size_t(buf.nbytes)) == 0
+    st = buf[:E, :8].astype(np.int64)
+    d = np.diff(st, axis=1)
+    t0 = st[:, 0].min()
+    res[E] = {
+        "median_cycles": {n: float(np.median(d[:, i])) for i, n in enumerate(names)},
+        "mean_cycles": {n: round(float(np.mean(d[:, i])), 1) for i, n in enumerate(names)},
+        "p90_cycles": {n: float(np.percentile(d[:, i], 90)) for i, n in enumerate(names)},
+        "wave_total_median": float(np.median(st[:, 7] - st[:, 0])),
+        "start_spread": float(np.percentile(st[:, 0] - t0, 90)),
+        "end_max_minus_first_start": float(st[:, 7].max() - t0),
+    }
+print(json.dumps(res, indent=1))

@@ -44,13 +44,15 @@ struct __align__(16) EnvScalars {
     double total;    // Environment.total_reward (fp64, as the reference's Python float)
 };
 
-// Per-package state byte: bits 0-1 env status (ST_*), then the persistent
+// Per-package state word (u16): bits 0-1 env status (ST_*), then the persistent
 // tracker's view of the same id (stale mode): present, in_transit, survivor
 // (inserted in an earlier episode -> its data lives in `trk`, not `pkg`).
-enum : uint32_t { PS_STATUS = 3u, PS_PRESENT = 4u, PS_TRANSIT = 8u, PS_SURVIVOR = 16u };
+enum : uint32_t { PS_STATUS = 3u, PS_PRESENT = 4u, PS_TRANSIT = 8u, PS_SURVIVOR = 16u, PS_FLAGS = 31u };
+// bits 5-15 of the state word: a survivor's dict-order rank (see ORD_EPISODE)
+constexpr int PS_RANK_SHIFT = 5;
 
 // Tracker iteration-order keys (stale mode), all < 0x800: a survivor's key is
-// its rank among the entries present at the last reset (stored in trk.z), an
+// its rank among the entries present at the last reset (pstate bits 5-15), an
 // entry of the running episode has ORD_EPISODE + slot (spawn order == id
 // order).  Dict order == ascending key.
 constexpr uint32_t ORD_EPISODE = 0x400u;
@@ -73,11 +75,11 @@ struct DevParams {
     // state (SoA, env-major)
     uint32_t* rob;             // [E][A] robot word, see rob_pack()
     uint64_t* pkg;             // [E][P] sr|sc<<8|tr<<16|tc<<24|st<<32|dl<<48 (cells packed r|c<<8)
-    uint8_t* pstate;           // [E][P] PS_* bits
+    uint16_t* pstate;          // [E][P] PS_* bits | survivor rank << PS_RANK_SHIFT
     EnvScalars* es;            // [E]
     uint32_t* mt;              // [E][624]
     int32_t* mt_pos;           // [E]
-    uint4* trk;                // [E][P] stale mode: (data lo, data hi, survivor order rank, 0)
+    uint64_t* trk;             // [E][P] stale mode: a tracker entry's data (written at insertion)
     double* ep_total;          // [E] total_reward of the last finished episode
     int32_t* ep_len;           // [E]
 };

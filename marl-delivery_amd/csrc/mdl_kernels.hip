@@ -125,9 +125,9 @@ __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[N
 // Reset with a persistent tracker: every present entry becomes a survivor
 // whose key is its rank in the current dict order (keys `tq`: survivor rank
 // or ORD_EPISODE + slot, distinct), so keys stay below ORD_EPISODE forever.
-// Returns the new ranks in `tq`; `renum` marks the entries to store.
+// The new rank lands in the state word's rank bits (and in `tq`).
 template <int NCH>
-__device__ inline void survivors_at_reset(uint32_t (&ps)[NCH], uint32_t (&tq)[NCH], bool (&renum)[NCH], int P) {
+__device__ inline void survivors_at_reset(uint32_t (&ps)[NCH], uint32_t (&tq)[NCH], int P) {
     const int lane = lane_id();
     uint32_t rk[NCH];
 #pragma unroll
@@ -144,10 +144,9 @@ __device__ inline void survivors_at_reset(uint32_t (&ps)[NCH], uint32_t (&tq)[NC
     }
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
-        renum[c] = c * WAVE + lane < P && (ps[c] & PS_PRESENT);
-        if (renum[c]) {
+        if (c * WAVE + lane < P && (ps[c] & PS_PRESENT)) {
             tq[c] = rk[c];
-            ps[c] |= PS_SURVIVOR;
+            ps[c] = (ps[c] & PS_FLAGS) | PS_SURVIVOR | (rk[c] << PS_RANK_SHIFT);
         } else {
             ps[c] &= PS_STATUS;
         }
@@ -211,19 +210,17 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restric
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
         ps[c] = j < P ? p.pstate[(size_t)e * P + j] : 0u;
-        tq[c] = ORD_EPISODE + (uint32_t)j;
-        if (p.stale && (ps[c] & PS_SURVIVOR)) tq[c] = p.trk[(size_t)e * P + j].z;
+        tq[c] = (p.stale && (ps[c] & PS_SURVIVOR)) ? ps[c] >> PS_RANK_SHIFT : ORD_EPISODE + (uint32_t)j;
     }
     const int cell = do_reset(p, e, md, L, false);
     uint64_t pk[NCH], td[NCH];
-    bool dirty[NCH], renum[NCH];
-    if (p.stale) survivors_at_reset<NCH>(ps, tq, renum, P);
+    bool dirty[NCH];
+    if (p.stale) survivors_at_reset<NCH>(ps, tq, P);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
         pk[c] = j < P ? L.pk[j] : 0;
         ps[c] = (j < P ? L.pst[j] : 0u) | (p.stale ? (ps[c] & ~PS_STATUS) : 0u);
-        if (!p.stale) renum[c] = false;
         td[c] = pk[c];
         dirty[c] = false;
     }
@@ -236,9 +233,8 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restric
         if (j < P) {
             const size_t g = (size_t)e * P + j;
             p.pkg[g] = pk[c];
-            p.pstate[g] = (uint8_t)ps[c];
-            if (dirty[c]) p.trk[g] = make_uint4((uint32_t)td[c], (uint32_t)(td[c] >> 32), 0u, 0u);
-            else if (renum[c]) reinterpret_cast<uint32_t*>(p.trk + g)[2] = tq[c];
+            p.pstate[g] = (uint16_t)ps[c];
+            if (dirty[c]) p.trk[g] = td[c];
         }
     }
     if (lane == 0) {
@@ -257,7 +253,7 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
     const int e = env_ids ? env_ids[w] : w;
     for (int j = lane_id(); j < p.P; j += WAVE) {
         const size_t g = (size_t)e * p.P + j;
-        p.pstate[g] &= (uint8_t)PS_STATUS;
+        p.pstate[g] &= (uint16_t)PS_STATUS;
     }
     if (lane_id() == 0) p.es[e].ctr = 0;
 }
@@ -279,9 +275,9 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     GLOBAL const uint8_t* mvalid = (GLOBAL const uint8_t*)p.movevalid;
     GLOBAL uint32_t* robp = (GLOBAL uint32_t*)p.rob;
     GLOBAL uint64_t* pkgp = (GLOBAL uint64_t*)p.pkg;
-    GLOBAL uint8_t* pstp = (GLOBAL uint8_t*)p.pstate;
+    GLOBAL uint16_t* pstp = (GLOBAL uint16_t*)p.pstate;
     GLOBAL u32x4* esp = (GLOBAL u32x4*)p.es;   // EnvScalars {t, ctr, total lo, total hi}
-    GLOBAL u32x4* trkp = (GLOBAL u32x4*)p.trk;
+    GLOBAL uint64_t* trkp = (GLOBAL uint64_t*)p.trk;
     int mW = p.maps[0].W, mgoff = p.maps[0].grid_off;
     GLOBAL const uint8_t* actp = (GLOBAL const uint8_t*)actions;
     GLOBAL const int* idsp = (GLOBAL const int*)env_ids;
@@ -323,11 +319,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             const size_t g = (size_t)e * P + j;
             pk[c] = pkgp[g];
             ps[c] = pstp[g];
-            if (STALE) {
-                const u32x4 v = trkp[g];
-                td[c] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-                tq[c] = v.z;
-            }
+            if (STALE) td[c] = trkp[g];
         }
         ps0[c] = ps[c];
     }
@@ -345,6 +337,8 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
             td[c] = pk[c];
             tq[c] = STALE ? ORD_EPISODE + (uint32_t)j : (uint32_t)j;
+        } else {
+            tq[c] = ps0[c] >> PS_RANK_SHIFT;
         }
     }
 
@@ -567,9 +561,6 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     // ---- reset on done (MAPPO/trainer.py:230-235) ----
     int t_out = t1;
     double total_out = total;
-    bool renum[NCH];
-#pragma unroll
-    for (int c = 0; c < NCH; c++) renum[c] = false;
     if (do_rst) {
         ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
         const MapDesc md = p.maps[mi];
@@ -579,7 +570,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             carry = 0;
             vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];
         }
-        if (STALE) survivors_at_reset<NCH>(ps, tq, renum, P);
+        if (STALE) survivors_at_reset<NCH>(ps, tq, P);
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const int j = c * WAVE + lane;
@@ -599,10 +590,9 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         const int j = c * WAVE + lane;
         if (j < P) {
             const size_t g = (size_t)e * P + j;
-            if (ps[c] != ps0[c]) pstp[g] = (uint8_t)ps[c];
+            if (ps[c] != ps0[c]) pstp[g] = (uint16_t)ps[c];
             if (do_rst) pkgp[g] = pk[c];
-            if (STALE && (dirty[c] || renum[c]))
-                trkp[g] = u32x4{(uint32_t)td[c], (uint32_t)(td[c] >> 32), renum[c] ? tq[c] : 0u, 0u};
+            if (STALE && dirty[c]) trkp[g] = td[c];
         }
     }
     if (lane == 0) {
@@ -673,17 +663,11 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
         const uint64_t d = p.pkg[g];
         const uint32_t f = p.pstate[g];
         S.pk[j] = d;
-        S.ps[j] = (uint8_t)f;
+        S.ps[j] = (uint8_t)(f & PS_FLAGS);
         if (STALE) {
-            uint64_t td = d;
-            uint32_t tq = ORD_EPISODE + (uint32_t)j;
-            if (f & PS_SURVIVOR) {
-                const uint4 v = p.trk[g];
-                td = (uint64_t)v.x | ((uint64_t)v.y << 32);
-                tq = v.z;
-            }
-            S.td[j] = td;
-            S.tq[j] = tq;
+            const bool sv = (f & PS_SURVIVOR) != 0;
+            S.td[j] = sv ? p.trk[g] : d;
+            S.tq[j] = sv ? f >> PS_RANK_SHIFT : ORD_EPISODE + (uint32_t)j;
         }
     }
     wave_sync();
@@ -862,9 +846,8 @@ __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict
             intr = (f & PS_TRANSIT) ? 1 : 0;
             order = ORD_EPISODE + (uint32_t)j;
             if (f & PS_SURVIVOR) {
-                const uint4 v = p.trk[g];
-                td = (uint64_t)v.x | ((uint64_t)v.y << 32);
-                order = v.z;
+                td = p.trk[g];
+                order = f >> PS_RANK_SHIFT;
             }
         } else {
             present = st == ST_WAITING || st == ST_IN_TRANSIT;

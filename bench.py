@@ -49,16 +49,18 @@ def parse():
     ap.add_argument("--T", type=int, default=500)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--graph-steps", type=int, default=100)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget per leg (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--fused-k", type=int, default=100, help="bench mode (ii): steps per fused launch (0 = skip)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches only (PMC profiling passes)")
     return ap.parse_args()
 
 
-def cpu_baseline(args, grid, seeds0, budget_s):
-    """The oracle's C restatement (single thread) on the same workload: the first
-    rank's envs, same seeds and the same action stream, for as many steps as fit
-    in ~budget_s of CPU time."""
+def cpu_baseline(args, grid, seeds0, budget_s, n_threads):
+    """The oracle's C restatement on the same workload: the first rank's envs,
+    same seeds and the same action stream, for as many steps as fit in
+    ~budget_s of wall time, on `n_threads` OpenMP threads (envs split
+    statically across threads, SURVEY.md §8(d) CPU leg (ii))."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     E, A = args.envs, args.agents
@@ -69,7 +71,7 @@ def cpu_baseline(args, grid, seeds0, budget_s):
     while t_all < budget_s:
         ints = torch.randint(0, 15, (E, A), generator=gen, dtype=torch.uint8).numpy()
         t0 = time.perf_counter()
-        ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS, n_threads=1)
+        ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS, n_threads=n_threads)
         t_all += time.perf_counter() - t0
         steps += 1
     cpu_model = platform.processor()
@@ -80,9 +82,19 @@ def cpu_baseline(args, grid, seeds0, budget_s):
                 break
     except OSError:
         pass
-    return {"value": E * A * steps / t_all, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+    how = "single thread" if n_threads == 1 else f"{n_threads} OpenMP threads"
+    return {"value": E * A * steps / t_all, "unit": "agent-steps/s", "cores": n_threads, "kind": "port",
             "sample": f"{E} envs x {steps} steps ({E * A * steps} agent-steps, {t_all:.1f} s) of the same workload, "
-                      f"oracle/mdl_oracle.c single thread, host {cpu_model}"}
+                      f"oracle/mdl_oracle.c, {how}, host {cpu_model}"}
+
+
+def cpu_threads():
+    """This process's CPU share: the affinity mask, capped at 16 (a one-GPU box's share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def main():
@@ -168,6 +180,23 @@ def main():
     barrier()
     wall_eager = time.perf_counter() - t1
 
+    # ---- bench mode: fused_k steps per launch, each env's
+    # state in registers between steps; same action stream; not the API path ----
+    wall_f, nf, Kf = None, 0, args.fused_k
+    if Kf > 0:
+        facts = acts.repeat((Kf + G - 1) // G, 1, 1)[:Kf].contiguous()
+        fr = torch.empty((Kf, E), dtype=torch.float64, device=dev)
+        fsh = torch.empty((Kf, E), dtype=torch.float32, device=dev)
+        fdn = torch.empty((Kf, E), dtype=torch.uint8, device=dev)
+        env.step_fused(facts, out=(fr, fsh, fdn))  # warm
+        nf = max(1, K // Kf)
+        barrier()
+        t2 = time.perf_counter()
+        for _ in range(nf):
+            env.step_fused(facts, out=(fr, fsh, fdn))
+        barrier()
+        wall_f = time.perf_counter() - t2
+
     # ---- per-launch kernel duration: HIP events on the launch stream around the
     # timed region (back-to-back launches, so this includes the ~1 us dispatch
     # gap between kernels and is an upper bound on the rocprof kernel time);
@@ -184,9 +213,10 @@ def main():
     kdur_iso_us = float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]) * 1e3)
 
     if dist is not None:
-        t = torch.tensor([wall, wall_eager], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall, wall_eager, wall_f or 0.0], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, wall_eager = float(t[0]), float(t[1])
+        wall_f = float(t[2]) if wall_f is not None else None
 
     total_agent_steps = E * A * K * world
     value = total_agent_steps / wall
@@ -201,9 +231,11 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
-        cpu = None
+        cpu = cpu1 = None
         if world == 1 and args.cpu_seconds > 0:
-            cpu = cpu_baseline(args, grid, seed0, args.cpu_seconds)
+            nt = cpu_threads()
+            cpu = cpu_baseline(args, grid, seed0, args.cpu_seconds, nt)
+            cpu1 = cpu if nt == 1 else cpu_baseline(args, grid, seed0, args.cpu_seconds, 1)
         out = {
             "metric": "agent-steps/sec (whole node), map1 5-agent 4096 envs, 1/2/4/8 MI355X",
             "value": value,
@@ -229,7 +261,13 @@ def main():
                          "kernel": "mdl::k_step<true, 1>", "kernel_us": kdur_us,
                          "kernel_us_isolated_event_pair": kdur_iso_us,
                          "algorithmic_bytes_per_launch": per_launch_bytes},
+            "fused_bench_mode": None if wall_f is None else {
+                "k_steps_per_launch": Kf, "launches": nf, "value": E * A * Kf * nf * world / wall_f,
+                "ms_per_step": wall_f / (Kf * nf) * 1e3,
+                "note": "SURVEY.md 8(d)(ii) bench mode: mdl_step_fused, K steps per launch on pre-generated device "
+                        "actions (bit-exact with K mdl_step calls); not the API path, not the headline value"},
             "cpu_baseline": cpu,
+            "cpu_baseline_1thread": cpu1,
         }
         print(json.dumps(out))
     if dist is not None:

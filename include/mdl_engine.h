@@ -90,6 +90,14 @@ int mdl_tracker_clear(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* s
 int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
              int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
 
+/* Bench mode: k_steps consecutive mdl_step calls fused
+ * into one launch, each env's state held in registers between steps.  Same
+ * results as k_steps mdl_step calls with actions[k] (bit-exact); actions are
+ * [k_steps][n][A], r_env / r_shaped / done are [k_steps][n].  Not part of the
+ * reference interface: a trainer needs the policy between steps. */
+int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
+                   int32_t k_steps, int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
+
 /* Observation builders for envs [env_begin, env_begin+n), which must share one
  * map shape (H, W), from the current state + tracker:
  *   actor_map  f32 [n][A][6][H][W]          convert_observation       MAPPO/helper.py:6-66

@@ -361,6 +361,22 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
     return 0;
 }
 
+int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
+                   int32_t k_steps, int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream) {
+    if (!eng || !actions) return fail("mdl_step_fused: null argument");
+    if (!eng->seeded) return fail("mdl_step_fused: engine not seeded (call mdl_seed first)");
+    if (action_format != MDL_ACTION_TRAINER_INT && action_format != MDL_ACTION_CODES)
+        return fail("mdl_step_fused: unknown action_format %d", action_format);
+    if (!env_ids) n = eng->p.E;
+    if (n < 0 || n > eng->p.E) return fail("mdl_step_fused: n=%d out of range", n);
+    if (k_steps < 1) return fail("mdl_step_fused: k_steps=%d must be >= 1", k_steps);
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_step_fused(eng->p, actions, action_format, env_ids, n, k_steps, auto_reset, r_env, r_shaped,
+                                  done, eng->wpb_step, eng->lds_step, (hipStream_t)stream));
+    return 0;
+}
+
 int mdl_build_obs(MdlEngine* eng, int32_t env_begin, int32_t n, float* actor_map, float* actor_vec,
                   float* critic_map, float* critic_vec, void* stream) {
     if (!eng) return fail("mdl_build_obs: null engine");

@@ -28,12 +28,16 @@
 
 namespace mdl {
 
-// Diagnostic build only (scripts/exp/stamps.sh): s_memtime per section of k_step.
+// Diagnostic build only (scripts/exp/stamps.py): s_memtime at section
+// boundaries of k_step, kept in SGPRs and stored once at the end; the
+// scheduling barriers keep every instruction inside its section.
 #ifdef MDL_STAMPS
 __device__ uint64_t g_stamps[65536 * 16];
-#define STAMP(k)                                                                          \
-    do {                                                                                  \
-        if (lane == 0) g_stamps[(size_t)w * 16 + (k)] = __builtin_amdgcn_s_memtime();     \
+#define STAMP(k)                                      \
+    do {                                              \
+        __builtin_amdgcn_sched_barrier(0);            \
+        stamp_[k] = __builtin_amdgcn_s_memtime();     \
+        __builtin_amdgcn_sched_barrier(0);            \
     } while (0)
 #else
 #define STAMP(k) \
@@ -259,12 +263,19 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 }
 
 // ------------------------------------------------------------------- step
-template <bool STALE, int NCH>
+// FUSED (bench mode): K consecutive steps of each env in
+// one launch with the state held in registers between them; actions [K][n][A],
+// outputs [K][n].  FUSED=false is the API's one step per launch (K = 1).
+template <bool STALE, int NCH, bool FUSED>
 __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __restrict__ actions, int fmt,
                                               const int* __restrict__ env_ids, int n, int auto_reset,
                                               double* __restrict__ r_out, float* __restrict__ sh_out,
-                                              uint8_t* __restrict__ done_out, int wpb, int lds_stride) {
+                                              uint8_t* __restrict__ done_out, int wpb, int lds_stride, int K) {
     extern __shared__ __align__(16) unsigned char smem[];
+#ifdef MDL_STAMPS
+    uint64_t stamp_[16];
+#endif
+    STAMP(0);
     // The kernel arguments the loads below need, fetched in one scalar batch
     // and pinned there (left alone, the compiler sinks each to its first use
     // and the wave pays one dependent scalar-cache miss per argument line).
@@ -286,6 +297,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     double* rop = r_out;
     pin(A); pin(P); pin(T); pin(env_map); pin(mvalid); pin(robp); pin(pkgp); pin(pstp); pin(esp); pin(trkp);
     pin(mW); pin(mgoff); pin(actp); pin(idsp); pin(fmt_); pin(n_); pin(wpb_); pin(c_touch); pin(rop);
+    STAMP(1);
 
     const int wave = wave_id();
     const int lane = lane_id();
@@ -299,13 +311,13 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         mgoff = p.maps[mi].grid_off;
     }
 
-    STAMP(0);
+    STAMP(2);
     // ---- loads: one round trip, everything independent ----
     const bool act = lane < A;
     const uint32_t rv = act ? robp[(size_t)e * A + lane] : 0u;
-    const int araw = act ? (int)actp[(size_t)w * A + lane] : 0;
+    int araw = act ? (int)actp[(size_t)w * A + lane] : 0;
     uint64_t pk[NCH], td[NCH];
-    uint32_t ps[NCH], ps0[NCH], tq[NCH];
+    uint32_t ps[NCH], ps_in[NCH], tq[NCH];
     bool dirty[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
@@ -321,268 +333,293 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             ps[c] = pstp[g];
             if (STALE) td[c] = trkp[g];
         }
-        ps0[c] = ps[c];
+        ps_in[c] = ps[c];
     }
     const u32x4 esv = esp[e];
     __builtin_amdgcn_sched_barrier(0);  // every load above is issued before any use
-    int mv = MV_S, op = 0;
-    if (act) decode_action(araw, fmt_, mv, op);
     int cell = rob_cell(rv), carry = rob_carry(rv);
     uint32_t vmask = rob_valid(rv);
-    const int t0 = (int)esv.x;
-    // tracker_prev view: data / iteration order key (< 0x800) per slot
+    int t_cur = (int)esv.x;
+    double tot_cur = __hiloint2double((int)esv.w, (int)esv.z);
+    bool any_rst = false;
+    const int KK = FUSED ? K : 1;
+    for (int k = 0; k < KK; k++) {
+        int mv = MV_S, op = 0;
+        if (act) decode_action(araw, fmt_, mv, op);
+        if (FUSED && k + 1 < KK) araw = act ? (int)actp[((size_t)(k + 1) * n_ + w) * A + lane] : 0;
+        const int t0 = t_cur;
+        uint32_t ps0[NCH];
 #pragma unroll
-    for (int c = 0; c < NCH; c++) {
-        const int j = c * WAVE + lane;
-        if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
-            td[c] = pk[c];
-            tq[c] = STALE ? ORD_EPISODE + (uint32_t)j : (uint32_t)j;
-        } else {
-            tq[c] = ps0[c] >> PS_RANK_SHIFT;
-        }
-    }
-
-    STAMP(1);
-    // ---- movement (env.py:188-257) ----
-    // moved = least fixed point of
-    //   moved[i] = mover[i] & winner(prop[i]) == i & (occ(prop[i]) none | moved[occ])
-    // winner = lowest-index mover into the cell: the reference's restart-from-0
-    // loop, checked against the oracle's literal restatement.
-    const int pcell = cell, pcarry = carry;
-    int prop = cell;
-    if (act && ((vmask >> mv) & 1u)) {  // bits 1..4 only: S / other moves never move
-        const int m = mv <= MV_R ? 256 : 1;  // L -256, R +256, U -1, D +1
-        prop = cell + ((mv & 1) ? -m : m);
-    }
-    const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
-    const uint64_t movers = ballot(mover);
-    uint64_t moved = 0;
-    if (movers) {
-        // blocked: a lower-index mover proposes the same cell; occ: the robot
-        // now standing on the proposed cell (robots stand on distinct cells)
-        int blocked = 0, occ = -1;
-        for (uint64_t m = movers; m; m &= m - 1) {
-            const int j = ffs64(m);
-            blocked |= (int)(j < lane) & (int)(rdl(prop, j) == prop);
-        }
-        for (int j = 0; j < A; j++) occ = rdl(cell, j) == prop ? j : occ;
-        const bool base = mover && !blocked;
-        for (int it = 0; it <= A; it++) {
-            const bool m = base && (occ < 0 || ((moved >> (occ & 63)) & 1ull));
-            const uint64_t nm = ballot(m);
-            if (nm == moved) break;
-            moved = nm;
-        }
-        if ((moved >> lane) & 1ull) {
-            cell = prop;
-            vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];  // consumed at write-back
-        }
-    }
-    const int n_cost = popc64(moved);
-
-    STAMP(2);
-    // ---- package actions (env.py:259-292); robots sit on distinct cells, so
-    // pick-ups and drops of different robots never interact ----
-    uint64_t pickers = ballot(!(MDL_ABLATE & 8) && act && op == 1 && carry == 0);
-    while (pickers) {
-        const int i = ffs64(pickers);
-        pickers &= pickers - 1;
-        const int ci = rdl(cell, i);
-        int found = -1;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            if (found < 0) {
-                const uint64_t b = ballot((ps[c] & PS_STATUS) == ST_WAITING && pk_start(pk[c]) == ci);
-                if (b) {
-                    const int jj = ffs64(b);
-                    found = c * WAVE + jj;
-                    if (lane == jj) ps[c] = (ps[c] & ~PS_STATUS) | ST_IN_TRANSIT;
-                }
-            }
-        }
-        if (found >= 0 && lane == i) carry = found + 1;
-    }
-    uint64_t droppers = ballot(!(MDL_ABLATE & 8) && act && op == 2 && carry != 0);
-    uint64_t dmask = 0, omask = 0;
-    while (droppers) {
-        const int i = ffs64(droppers);
-        droppers &= droppers - 1;
-        const int j = rdl(carry, i) - 1;
-        const int ci = rdl(cell, i);
-        const int cc = j >> 6, jj = j & 63;
-        uint64_t v = 0;
-#pragma unroll
-        for (int c = 0; c < NCH; c++)
-            if (c == cc) v = pk[c];
-        const uint64_t d = (uint64_t)(uint32_t)rdl((int)(uint32_t)v, jj) |
-                           ((uint64_t)(uint32_t)rdl((int)(uint32_t)(v >> 32), jj) << 32);
-        if (pk_target(d) == ci) {
-            dmask |= 1ull << i;
-            if (t0 <= pk_dl(d)) omask |= 1ull << i;
-#pragma unroll
-            for (int c = 0; c < NCH; c++)
-                if (c == cc && lane == jj) ps[c] = (ps[c] & ~PS_STATUS) | ST_DELIVERED;
-            if (lane == i) carry = 0;
-        }
-    }
-    // reward: fp64 fold in the reference's order (move costs, then deliveries)
-    double rr = 0.0;
-    for (int k = 0; k < n_cost; k++) rr += p.move_cost;
-    for (uint64_t m = dmask; m; m &= m - 1) {
-        const int i = ffs64(m);
-        rr += ((omask >> i) & 1ull) ? p.delivery_reward : p.delay_reward;
-    }
-    const int t1 = t0 + 1;
-    const double total = __hiloint2double((int)esv.w, (int)esv.z) + rr;
-
-    STAMP(3);
-    // ---- terminate (env.py:308-316) + spawn (get_state env.py:133-137) ----
-    int ndel = 0;
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-        const int j = c * WAVE + lane;
-        ndel += popc64(ballot((ps[c] & PS_STATUS) == ST_DELIVERED));
-        if (j < P && pk_st(pk[c]) == t1) ps[c] = (ps[c] & ~PS_STATUS) | ST_WAITING;
-    }
-    const bool done = (t1 == T) || (ndel == P);
-
-    STAMP(4);
-    // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
-    // Agents on lanes.  Each agent that needs the nearest waiting package of
-    // tracker_prev (st <= t_prev) gets it from one DPP minimum over the package
-    // lanes of (distance << 11 | order key); idle-nearby is that distance <= 3.
-    // The reference's if-chains become selects: adding 0.0f is exact here
-    // (s starts at +0 and never becomes -0).
-    float s_lane = 0.0f;
-    if (!(MDL_ABLATE & 1)) {
-        // tracker_prev entry of each agent's previously carried id (ds_bpermute gather)
-        const int pj = pcarry - 1;
-        uint32_t pf = 0;
-        uint64_t pdat = 0;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            const int src = (pj & 63) << 2;
-            const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ps0[c]);
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)td[c]);
-            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(td[c] >> 32));
-            if ((pj >> 6) == c) {
-                pf = f;
-                pdat = (uint64_t)lo | ((uint64_t)hi << 32);
-            }
-        }
-        const bool ppres = act && pcarry != 0 && pcarry <= P &&
-                           (STALE ? (pf & PS_PRESENT) != 0
-                                  : ((pf & PS_STATUS) == ST_WAITING || (pf & PS_STATUS) == ST_IN_TRANSIT));
-        const bool moved_a = pcell != cell;
-        const bool need_near = act && moved_a && !(pcarry != 0 && ppres);
-        const bool need_idle = act && !moved_a && mv == MV_S && pcarry == 0;
-        const bool need_can = act && op == 1 && pcarry == 0 && carry == 0;
-        bool wv[NCH];
-        int stc[NCH];
-        uint64_t anyw = 0;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            const uint32_t f = ps0[c];
-            const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
-            wv[c] = waiting && pk_st(td[c]) <= t0;
-            stc[c] = pk_start(td[c]);
-            anyw |= ballot(wv[c]);
-        }
-        // per-agent answers: bit masks in SGPRs, the nearest start cell written
-        // into the agent's lane
-        uint64_t idle_m = 0, can_m = 0;
-        int best_cell = -1;
-        if (anyw) {
-            for (uint64_t q = ballot(need_near || need_idle); q; q &= q - 1) {
-                const int a = ffs64(q);
-                const int pa = rdl(pcell, a);
-                uint32_t key[NCH];
-                uint32_t kmin = 0xffffffffu;
-#pragma unroll
-                for (int c = 0; c < NCH; c++) {
-                    key[c] = wv[c] ? ((uint32_t)manhattan(pa, stc[c]) << 11) | tq[c] : 0xffffffffu;
-                    const uint32_t m = wave_min_u32(key[c]);
-                    kmin = m < kmin ? m : kmin;
-                }
-                int bc = -1;
-#pragma unroll
-                for (int c = 0; c < NCH; c++) {
-                    const uint64_t b = ballot(key[c] == kmin);
-                    const int v = rdl(stc[c], ffs64(b) & 63);
-                    bc = b ? v : bc;
-                }
-                idle_m |= (uint64_t)((kmin >> 11) <= 3u) << a;
-                best_cell = lane == a ? bc : best_cell;
-            }
-            for (uint64_t q = ballot(need_can); q; q &= q - 1) {
-                const int a = ffs64(q);
-                const int ca = rdl(cell, a);
-                uint64_t h = 0;
-#pragma unroll
-                for (int c = 0; c < NCH; c++) h |= ballot(wv[c] && stc[c] == ca);
-                can_m |= (uint64_t)(h != 0) << a;
-            }
-        }
-        const bool idle = (idle_m >> lane) & 1ull, can = (can_m >> lane) & 1ull;
-        // the constants, pinned in SGPRs so the selects below stay branch-free
-        float cs[9];
-#pragma unroll
-        for (int k = 0; k < 9; k++) {
-            cs[k] = p.shaping[k];
-            pin(cs[k]);
-        }
-        const int ptg = pk_target(pdat);
-        float s = 0.0f;
-        // 1. pickup / delivery
-        const bool pick = pcarry == 0 && carry != 0;
-        const bool deliv = pcarry != 0 && carry == 0 && ppres && cell == ptg;
-        s = s + (pick ? cs[SH_PICK] : deliv ? ((t1 <= pk_dl(pdat)) ? cs[SH_ONTIME] : cs[SH_LATE]) : 0.0f);
-        // 2. wasted operations
-        const bool wpick = op == 1 && (pcarry != 0 || (carry == 0 && !can));
-        const bool wdrop = op == 2 && (pcarry == 0 || (carry != 0 && ppres && cell != ptg));
-        s = s + (wpick ? cs[SH_WPICK] : wdrop ? cs[SH_WDROP] : 0.0f);
-        // 3. movement
-        s = s + ((mv != MV_S && !moved_a) ? cs[SH_STUCK] : 0.0f);
-        const int tgt = (pcarry != 0 && ppres) ? ptg : best_cell;
-        const int db = manhattan(pcell, tgt), da = manhattan(cell, tgt);
-        s = s + ((tgt >= 0 && moved_a) ? (da < db ? cs[SH_CLOSER] : da > db ? cs[SH_AWAY] : 0.0f) : 0.0f);
-        // 4. idle next to an available package
-        s = s + ((!moved_a && mv == MV_S && pcarry == 0 && idle) ? cs[SH_IDLE] : 0.0f);
-        s_lane = act ? s : 0.0f;
-    }
-    const float shaped = (float)rr + np_sum_lanes(s_lane, A);
-
-    STAMP(5);
-    // ---- tracker update with the new state; a done env that resets here skips
-    // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
-    const bool do_rst = done && auto_reset;
-    if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, carry, t1);
-
-    // ---- reset on done (MAPPO/trainer.py:230-235) ----
-    int t_out = t1;
-    double total_out = total;
-    if (do_rst) {
-        ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
-        const MapDesc md = p.maps[mi];
-        const int nc = do_reset(p, e, md, L, false);
-        if (act) {
-            cell = nc;
-            carry = 0;
-            vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];
-        }
-        if (STALE) survivors_at_reset<NCH>(ps, tq, P);
+        for (int c = 0; c < NCH; c++) ps0[c] = ps[c];
+        // tracker_prev view: data / iteration order key (< 0x800) per slot
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const int j = c * WAVE + lane;
-            pk[c] = j < P ? L.pk[j] : 0;
-            ps[c] = (j < P ? L.pst[j] : 0u) | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
+            if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
+                td[c] = pk[c];
+                tq[c] = STALE ? ORD_EPISODE + (uint32_t)j : (uint32_t)j;
+            } else {
+                tq[c] = ps0[c] >> PS_RANK_SHIFT;
+            }
         }
-        if (STALE) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, 0, 0);
-        t_out = 0;
-        total_out = 0.0;
-    }
 
-    STAMP(6);
+        STAMP(3);
+        // ---- movement (env.py:188-257) ----
+        // moved = least fixed point of
+        //   moved[i] = mover[i] & winner(prop[i]) == i & (occ(prop[i]) none | moved[occ])
+        // winner = lowest-index mover into the cell: the reference's restart-from-0
+        // loop, checked against the oracle's literal restatement.
+        const int pcell = cell, pcarry = carry;
+        int prop = cell;
+        if (act && ((vmask >> mv) & 1u)) {  // bits 1..4 only: S / other moves never move
+            const int m = mv <= MV_R ? 256 : 1;  // L -256, R +256, U -1, D +1
+            prop = cell + ((mv & 1) ? -m : m);
+        }
+        const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
+        const uint64_t movers = ballot(mover);
+        uint64_t moved = 0;
+        if (movers) {
+            // blocked: a lower-index mover proposes the same cell; occ: the robot
+            // now standing on the proposed cell (robots stand on distinct cells)
+            int blocked = 0, occ = -1;
+            for (uint64_t m = movers; m; m &= m - 1) {
+                const int j = ffs64(m);
+                blocked |= (int)(j < lane) & (int)(rdl(prop, j) == prop);
+            }
+            for (int j = 0; j < A; j++) occ = rdl(cell, j) == prop ? j : occ;
+            const bool base = mover && !blocked;
+            for (int it = 0; it <= A; it++) {
+                const bool m = base && (occ < 0 || ((moved >> (occ & 63)) & 1ull));
+                const uint64_t nm = ballot(m);
+                if (nm == moved) break;
+                moved = nm;
+            }
+            if ((moved >> lane) & 1ull) {
+                cell = prop;
+                vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];  // consumed at write-back
+            }
+        }
+        const int n_cost = popc64(moved);
+
+        STAMP(4);
+        // ---- package actions (env.py:259-292); robots sit on distinct cells, so
+        // pick-ups and drops of different robots never interact ----
+        uint64_t pickers = ballot(!(MDL_ABLATE & 8) && act && op == 1 && carry == 0);
+        while (pickers) {
+            const int i = ffs64(pickers);
+            pickers &= pickers - 1;
+            const int ci = rdl(cell, i);
+            int found = -1;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                if (found < 0) {
+                    const uint64_t b = ballot((ps[c] & PS_STATUS) == ST_WAITING && pk_start(pk[c]) == ci);
+                    if (b) {
+                        const int jj = ffs64(b);
+                        found = c * WAVE + jj;
+                        if (lane == jj) ps[c] = (ps[c] & ~PS_STATUS) | ST_IN_TRANSIT;
+                    }
+                }
+            }
+            if (found >= 0 && lane == i) carry = found + 1;
+        }
+        uint64_t droppers = ballot(!(MDL_ABLATE & 8) && act && op == 2 && carry != 0);
+        uint64_t dmask = 0, omask = 0;
+        while (droppers) {
+            const int i = ffs64(droppers);
+            droppers &= droppers - 1;
+            const int j = rdl(carry, i) - 1;
+            const int ci = rdl(cell, i);
+            const int cc = j >> 6, jj = j & 63;
+            uint64_t v = 0;
+#pragma unroll
+            for (int c = 0; c < NCH; c++)
+                if (c == cc) v = pk[c];
+            const uint64_t d = (uint64_t)(uint32_t)rdl((int)(uint32_t)v, jj) |
+                               ((uint64_t)(uint32_t)rdl((int)(uint32_t)(v >> 32), jj) << 32);
+            if (pk_target(d) == ci) {
+                dmask |= 1ull << i;
+                if (t0 <= pk_dl(d)) omask |= 1ull << i;
+#pragma unroll
+                for (int c = 0; c < NCH; c++)
+                    if (c == cc && lane == jj) ps[c] = (ps[c] & ~PS_STATUS) | ST_DELIVERED;
+                if (lane == i) carry = 0;
+            }
+        }
+        // reward: fp64 fold in the reference's order (move costs, then deliveries)
+        double rr = 0.0;
+        for (int k = 0; k < n_cost; k++) rr += p.move_cost;
+        for (uint64_t m = dmask; m; m &= m - 1) {
+            const int i = ffs64(m);
+            rr += ((omask >> i) & 1ull) ? p.delivery_reward : p.delay_reward;
+        }
+        const int t1 = t0 + 1;
+        const double total = tot_cur + rr;
+
+        STAMP(5);
+        // ---- terminate (env.py:308-316) + spawn (get_state env.py:133-137) ----
+        int ndel = 0;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const int j = c * WAVE + lane;
+            ndel += popc64(ballot((ps[c] & PS_STATUS) == ST_DELIVERED));
+            if (j < P && pk_st(pk[c]) == t1) ps[c] = (ps[c] & ~PS_STATUS) | ST_WAITING;
+        }
+        const bool done = (t1 == T) || (ndel == P);
+
+        STAMP(6);
+        // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
+        // Agents on lanes.  Each agent that needs the nearest waiting package of
+        // tracker_prev (st <= t_prev) gets it from one DPP minimum over the package
+        // lanes of (distance << 11 | order key); idle-nearby is that distance <= 3.
+        // The reference's if-chains become selects: adding 0.0f is exact here
+        // (s starts at +0 and never becomes -0).
+        float s_lane = 0.0f;
+        if (!(MDL_ABLATE & 1)) {
+            // tracker_prev entry of each agent's previously carried id (ds_bpermute gather)
+            const int pj = pcarry - 1;
+            uint32_t pf = 0;
+            uint64_t pdat = 0;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                const int src = (pj & 63) << 2;
+                const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ps0[c]);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)td[c]);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(td[c] >> 32));
+                if ((pj >> 6) == c) {
+                    pf = f;
+                    pdat = (uint64_t)lo | ((uint64_t)hi << 32);
+                }
+            }
+            const bool ppres = act && pcarry != 0 && pcarry <= P &&
+                               (STALE ? (pf & PS_PRESENT) != 0
+                                      : ((pf & PS_STATUS) == ST_WAITING || (pf & PS_STATUS) == ST_IN_TRANSIT));
+            const bool moved_a = pcell != cell;
+            const bool need_near = act && moved_a && !(pcarry != 0 && ppres);
+            const bool need_idle = act && !moved_a && mv == MV_S && pcarry == 0;
+            const bool need_can = act && op == 1 && pcarry == 0 && carry == 0;
+            bool wv[NCH];
+            int stc[NCH];
+            uint64_t anyw = 0;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                const uint32_t f = ps0[c];
+                const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
+                wv[c] = waiting && pk_st(td[c]) <= t0;
+                stc[c] = pk_start(td[c]);
+                anyw |= ballot(wv[c]);
+            }
+            STAMP(7);
+            // per-agent answers: bit masks in SGPRs, the nearest start cell written
+            // into the agent's lane
+            uint64_t idle_m = 0, can_m = 0;
+            int best_cell = -1;
+            if (anyw) {
+                for (uint64_t q = ballot(need_near || need_idle); q; q &= q - 1) {
+                    const int a = ffs64(q);
+                    const int pa = rdl(pcell, a);
+                    uint32_t key[NCH];
+                    uint32_t kmin = 0xffffffffu;
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        key[c] = wv[c] ? ((uint32_t)manhattan(pa, stc[c]) << 11) | tq[c] : 0xffffffffu;
+                        const uint32_t m = wave_min_u32(key[c]);
+                        kmin = m < kmin ? m : kmin;
+                    }
+                    int bc = -1;
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        const uint64_t b = ballot(key[c] == kmin);
+                        const int v = rdl(stc[c], ffs64(b) & 63);
+                        bc = b ? v : bc;
+                    }
+                    idle_m |= (uint64_t)((kmin >> 11) <= 3u) << a;
+                    best_cell = lane == a ? bc : best_cell;
+                }
+                for (uint64_t q = ballot(need_can); q; q &= q - 1) {
+                    const int a = ffs64(q);
+                    const int ca = rdl(cell, a);
+                    uint64_t h = 0;
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) h |= ballot(wv[c] && stc[c] == ca);
+                    can_m |= (uint64_t)(h != 0) << a;
+                }
+            }
+            const bool idle = (idle_m >> lane) & 1ull, can = (can_m >> lane) & 1ull;
+            STAMP(8);
+            // the constants, pinned in SGPRs so the selects below stay branch-free
+            float cs[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                cs[k] = p.shaping[k];
+                pin(cs[k]);
+            }
+            const int ptg = pk_target(pdat);
+            float s = 0.0f;
+            // 1. pickup / delivery
+            const bool pick = pcarry == 0 && carry != 0;
+            const bool deliv = pcarry != 0 && carry == 0 && ppres && cell == ptg;
+            s = s + (pick ? cs[SH_PICK] : deliv ? ((t1 <= pk_dl(pdat)) ? cs[SH_ONTIME] : cs[SH_LATE]) : 0.0f);
+            // 2. wasted operations
+            const bool wpick = op == 1 && (pcarry != 0 || (carry == 0 && !can));
+            const bool wdrop = op == 2 && (pcarry == 0 || (carry != 0 && ppres && cell != ptg));
+            s = s + (wpick ? cs[SH_WPICK] : wdrop ? cs[SH_WDROP] : 0.0f);
+            // 3. movement
+            s = s + ((mv != MV_S && !moved_a) ? cs[SH_STUCK] : 0.0f);
+            const int tgt = (pcarry != 0 && ppres) ? ptg : best_cell;
+            const int db = manhattan(pcell, tgt), da = manhattan(cell, tgt);
+            s = s + ((tgt >= 0 && moved_a) ? (da < db ? cs[SH_CLOSER] : da > db ? cs[SH_AWAY] : 0.0f) : 0.0f);
+            // 4. idle next to an available package
+            s = s + ((!moved_a && mv == MV_S && pcarry == 0 && idle) ? cs[SH_IDLE] : 0.0f);
+            s_lane = act ? s : 0.0f;
+        }
+        const float shaped = (float)rr + np_sum_lanes(s_lane, A);
+
+        STAMP(9);
+        // ---- tracker update with the new state; a done env that resets here skips
+        // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
+        const bool do_rst = done && auto_reset;
+        if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, carry, t1);
+
+        // ---- reset on done (MAPPO/trainer.py:230-235) ----
+        int t_out = t1;
+        double total_out = total;
+        if (do_rst) {
+            ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
+            const MapDesc md = p.maps[mi];
+            const int nc = do_reset(p, e, md, L, false);
+            if (act) {
+                cell = nc;
+                carry = 0;
+                vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];
+            }
+            if (STALE) survivors_at_reset<NCH>(ps, tq, P);
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                const int j = c * WAVE + lane;
+                pk[c] = j < P ? L.pk[j] : 0;
+                ps[c] = (j < P ? L.pst[j] : 0u) | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
+            }
+            if (STALE) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, 0, 0);
+            t_out = 0;
+            total_out = 0.0;
+            any_rst = true;
+        }
+        t_cur = t_out;
+        tot_cur = total_out;
+        if (lane == 0) {
+            if (done) {
+                p.ep_total[e] = total;
+                p.ep_len[e] = t1;
+            }
+            const size_t o = (size_t)k * n_ + w;
+            if (rop) rop[o] = rr;
+            if (sh_out) sh_out[o] = shaped;
+            if (done_out) done_out[o] = done ? 1 : 0;
+        }
+    }  // steps
+
+    STAMP(10);
     // ---- write back only what changed ----
     if (act) robp[(size_t)e * A + lane] = rob_pack(cell, carry, vmask);
 #pragma unroll
@@ -590,22 +627,18 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
         const int j = c * WAVE + lane;
         if (j < P) {
             const size_t g = (size_t)e * P + j;
-            if (ps[c] != ps0[c]) pstp[g] = (uint16_t)ps[c];
-            if (do_rst) pkgp[g] = pk[c];
+            if (ps[c] != ps_in[c]) pstp[g] = (uint16_t)ps[c];
+            if (any_rst) pkgp[g] = pk[c];
             if (STALE && dirty[c]) trkp[g] = td[c];
         }
     }
-    if (lane == 0) {
-        esp[e] = u32x4{(uint32_t)t_out, 0u, (uint32_t)__double2loint(total_out), (uint32_t)__double2hiint(total_out)};
-        if (done) {
-            p.ep_total[e] = total;
-            p.ep_len[e] = t1;
-        }
-        if (rop) rop[w] = rr;
-        if (sh_out) sh_out[w] = shaped;
-        if (done_out) done_out[w] = done ? 1 : 0;
-    }
-    STAMP(7);
+    if (lane == 0)
+        esp[e] = u32x4{(uint32_t)t_cur, 0u, (uint32_t)__double2loint(tot_cur), (uint32_t)__double2hiint(tot_cur)};
+    STAMP(11);
+#ifdef MDL_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < 12; k++) g_stamps[(size_t)w * 16 + k] = stamp_[k];
+#endif
 }
 
 // ------------------------------------------------------------- observations
@@ -906,29 +939,37 @@ hipError_t launch_tracker_clear(const DevParams& p, const int* ids, int n, hipSt
     return hipGetLastError();
 }
 
-template <bool ST, int NCH>
+template <bool ST, int NCH, bool FUSED>
 static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
-                          double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((k_step<ST, NCH>), dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, actions, fmt, ids, n,
-                       auto_reset, r, sh, done, wpb, (int)lds);
+                          double* r, float* sh, uint8_t* done, int wpb, size_t lds, int K, hipStream_t s) {
+    hipLaunchKernelGGL((k_step<ST, NCH, FUSED>), dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, actions, fmt,
+                       ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
 }
 
-template <bool ST>
+template <bool ST, bool FUSED>
 static void launch_step_s(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
-                          double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
+                          double* r, float* sh, uint8_t* done, int wpb, size_t lds, int K, hipStream_t s) {
     switch (nch_for(p.P)) {
-        case 1: launch_step_t<ST, 1>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
-        case 2: launch_step_t<ST, 2>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
-        case 4: launch_step_t<ST, 4>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
-        case 8: launch_step_t<ST, 8>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
-        default: launch_step_t<ST, 16>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s); break;
+        case 1: launch_step_t<ST, 1, FUSED>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s); break;
+        case 2: launch_step_t<ST, 2, FUSED>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s); break;
+        case 4: launch_step_t<ST, 4, FUSED>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s); break;
+        case 8: launch_step_t<ST, 8, FUSED>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s); break;
+        default: launch_step_t<ST, 16, FUSED>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s); break;
     }
 }
 
 hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
                        double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
-    if (p.stale) launch_step_s<true>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s);
-    else launch_step_s<false>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, s);
+    if (p.stale) launch_step_s<true, false>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, 1, s);
+    else launch_step_s<false, false>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, 1, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int K,
+                             int auto_reset, double* r, float* sh, uint8_t* done, int wpb, size_t lds,
+                             hipStream_t s) {
+    if (p.stale) launch_step_s<true, true>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s);
+    else launch_step_s<false, true>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s);
     return hipGetLastError();
 }
 

@@ -54,6 +54,7 @@ SIGNATURES = {
     "mdl_reset": (C.c_int, [_vp, _vp, _i32, _vp]),
     "mdl_tracker_clear": (C.c_int, [_vp, _vp, _i32, _vp]),
     "mdl_step": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "mdl_step_fused": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mdl_build_obs": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mdl_read_state": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mdl_views_features": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32,

@@ -174,6 +174,30 @@ class BatchedEnv:
         self._keep = (ids, actions)
         return r, sh, d
 
+    def step_fused(self, actions: torch.Tensor, env_ids=None, auto_reset: bool = True, action_format: str = "int",
+                   out=None):
+        """Bench mode: K consecutive steps in one launch.
+
+        actions: uint8 [K, n, A]; returns (r_env f64 [K, n], r_shaped f32 [K, n],
+        done uint8 [K, n]), identical to K ``step`` calls with actions[k].
+        """
+        ids, n = self._ids(env_ids)
+        if actions.dtype != torch.uint8 or actions.device != self.device or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=torch.uint8).contiguous()
+        if actions.dim() != 3 or actions.shape[1] != n or actions.shape[2] != self.A:
+            raise ValueError(f"actions must be [K, {n}, {self.A}]")
+        K = actions.shape[0]
+        if out is None:
+            r = torch.empty((K, n), dtype=torch.float64, device=self.device)
+            sh = torch.empty((K, n), dtype=torch.float32, device=self.device)
+            d = torch.empty((K, n), dtype=torch.uint8, device=self.device)
+        else:
+            r, sh, d = out
+        check(lib().mdl_step_fused(self._h, ptr(actions), ACTION_FORMATS[action_format], ptr(ids), n, K,
+                                   int(bool(auto_reset)), ptr(r), ptr(sh), ptr(d), self._stream()), "mdl_step_fused")
+        self._keep = (ids, actions)
+        return r, sh, d
+
     def obs_buffers(self, n=None, H=None, W=None):
         n = self.E if n is None else n
         H = self.grids[0].shape[0] if H is None else H

@@ -21,7 +21,8 @@
 #include "mdl_features.hpp"
 
 // Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
-// reward, 2 the tracker update, 4 movement, 8 package actions.  0 in the product.
+// reward, 2 the tracker update, 4 movement, 8 package actions, 16 the move-validity
+// reload, 32 the shaping agent loops, 64 the carried-package gather.  0 in the product.
 #ifndef MDL_ABLATE
 #define MDL_ABLATE 0
 #endif
@@ -266,8 +267,13 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 // FUSED (bench mode): K consecutive steps of each env in
 // one launch with the state held in registers between them; actions [K][n][A],
 // outputs [K][n].  FUSED=false is the API's one step per launch (K = 1).
+#ifndef MDL_STEP_WPB
+#define MDL_STEP_LB 256
+#else
+#define MDL_STEP_LB (64 * MDL_STEP_WPB)
+#endif
 template <bool STALE, int NCH, bool FUSED>
-__global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __restrict__ actions, int fmt,
+__global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t* __restrict__ actions, int fmt,
                                               const int* __restrict__ env_ids, int n, int auto_reset,
                                               double* __restrict__ r_out, float* __restrict__ sh_out,
                                               uint8_t* __restrict__ done_out, int wpb, int lds_stride, int K) {
@@ -283,7 +289,6 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     // read later (constants, output pointers) hit the scalar cache.
     int A = p.A, P = p.P, T = p.T;
     GLOBAL const uint8_t* env_map = (GLOBAL const uint8_t*)p.env_map;
-    GLOBAL const uint8_t* mvalid = (GLOBAL const uint8_t*)p.movevalid;
     GLOBAL uint32_t* robp = (GLOBAL uint32_t*)p.rob;
     GLOBAL uint64_t* pkgp = (GLOBAL uint64_t*)p.pkg;
     GLOBAL uint16_t* pstp = (GLOBAL uint16_t*)p.pstate;
@@ -294,9 +299,11 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
     GLOBAL const int* idsp = (GLOBAL const int*)env_ids;
     int fmt_ = fmt, n_ = n, wpb_ = wpb;
     float c_touch = p.shaping[8];
-    double* rop = r_out;
-    pin(A); pin(P); pin(T); pin(env_map); pin(mvalid); pin(robp); pin(pkgp); pin(pstp); pin(esp); pin(trkp);
-    pin(mW); pin(mgoff); pin(actp); pin(idsp); pin(fmt_); pin(n_); pin(wpb_); pin(c_touch); pin(rop);
+    const uint8_t* c_touch2 = p.movevalid;
+    double* c_touch3 = r_out;
+    pin(A); pin(P); pin(T); pin(env_map); pin(robp); pin(pkgp); pin(pstp); pin(esp); pin(trkp);
+    pin(mW); pin(mgoff); pin(actp); pin(idsp); pin(fmt_); pin(n_); pin(wpb_); pin(c_touch); pin(c_touch2);
+    pin(c_touch3);
     STAMP(1);
 
     const int wave = wave_id();
@@ -396,7 +403,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             }
             if ((moved >> lane) & 1ull) {
                 cell = prop;
-                vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];  // consumed at write-back
+                if (!(MDL_ABLATE & 16)) vmask = p.movevalid[mgoff + cell_r(cell) * mW + cell_c(cell)];  // consumed at write-back
             }
         }
         const int n_cost = popc64(moved);
@@ -481,7 +488,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             uint32_t pf = 0;
             uint64_t pdat = 0;
 #pragma unroll
-            for (int c = 0; c < NCH; c++) {
+            for (int c = 0; c < NCH && !(MDL_ABLATE & 64); c++) {
                 const int src = (pj & 63) << 2;
                 const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ps0[c]);
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)td[c]);
@@ -514,7 +521,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             // into the agent's lane
             uint64_t idle_m = 0, can_m = 0;
             int best_cell = -1;
-            if (anyw) {
+            if (anyw && !(MDL_ABLATE & 32)) {
                 for (uint64_t q = ballot(need_near || need_idle); q; q &= q - 1) {
                     const int a = ffs64(q);
                     const int pa = rdl(pcell, a);
@@ -591,7 +598,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
             if (act) {
                 cell = nc;
                 carry = 0;
-                vmask = mvalid[mgoff + cell_r(cell) * mW + cell_c(cell)];
+                vmask = p.movevalid[mgoff + cell_r(cell) * mW + cell_c(cell)];
             }
             if (STALE) survivors_at_reset<NCH>(ps, tq, P);
 #pragma unroll
@@ -613,7 +620,7 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
                 p.ep_len[e] = t1;
             }
             const size_t o = (size_t)k * n_ + w;
-            if (rop) rop[o] = rr;
+            if (r_out) r_out[o] = rr;
             if (sh_out) sh_out[o] = shaped;
             if (done_out) done_out[o] = done ? 1 : 0;
         }
@@ -621,19 +628,21 @@ __global__ __launch_bounds__(256) void k_step(DevParams p, const uint8_t* __rest
 
     STAMP(10);
     // ---- write back only what changed ----
-    if (act) robp[(size_t)e * A + lane] = rob_pack(cell, carry, vmask);
+    // (through the kernel arguments again, not the pinned copies above, so no
+    // pointer stays live in SGPRs across the step)
+    if (act) p.rob[(size_t)e * A + lane] = rob_pack(cell, carry, vmask);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
         if (j < P) {
             const size_t g = (size_t)e * P + j;
-            if (ps[c] != ps_in[c]) pstp[g] = (uint16_t)ps[c];
-            if (any_rst) pkgp[g] = pk[c];
-            if (STALE && dirty[c]) trkp[g] = td[c];
+            if (ps[c] != ps_in[c]) p.pstate[g] = (uint16_t)ps[c];
+            if (any_rst) p.pkg[g] = pk[c];
+            if (STALE && dirty[c]) p.trk[g] = td[c];
         }
     }
     if (lane == 0)
-        esp[e] = u32x4{(uint32_t)t_cur, 0u, (uint32_t)__double2loint(tot_cur), (uint32_t)__double2hiint(tot_cur)};
+        ((u32x4*)p.es)[e] = u32x4{(uint32_t)t_cur, 0u, (uint32_t)__double2loint(tot_cur), (uint32_t)__double2hiint(tot_cur)};
     STAMP(11);
 #ifdef MDL_STAMPS
     if (lane == 0)
@@ -942,8 +951,14 @@ hipError_t launch_tracker_clear(const DevParams& p, const int* ids, int n, hipSt
 template <bool ST, int NCH, bool FUSED>
 static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
                           double* r, float* sh, uint8_t* done, int wpb, size_t lds, int K, hipStream_t s) {
+#ifdef MDL_STEP_WPB  // profiling builds only: workgroup shape experiments
+    wpb = MDL_STEP_WPB;
+    hipLaunchKernelGGL((k_step<ST, NCH, FUSED>), dim3(blocks_for(n, wpb)), dim3(64 * wpb), lds * wpb, s, p, actions,
+                       fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+#else
     hipLaunchKernelGGL((k_step<ST, NCH, FUSED>), dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, actions, fmt,
                        ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+#endif
 }
 
 template <bool ST, bool FUSED>

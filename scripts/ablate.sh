@@ -3,8 +3,8 @@
 set -e
 cd "$(dirname "$0")/../marl-delivery_amd"
 mkdir -p build/ablate
-for A in 0 1 2 3 4 8 15; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -DMDL_ABLATE=$A \
+for A in ${VARIANTS:-0 1 2 3 4 8 15}; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -DMDL_ABLATE=$A \
      -I../include -Icsrc -shared csrc/mdl_kernels.hip csrc/mdl_engine.hip -o build/ablate/libmdl_$A.so &
 done
 wait

@@ -11,7 +11,7 @@ L = C.CDLL(os.path.join(here, "libexp.so"))
 dev = torch.device("cuda", 0)
 s = torch.cuda.Stream()
 out = {}
-for E in (1024, 2048, 4096, 8192, 16384):
+for E in (1024, 4096, 16384):
     A, P = 5, 50
     rob = torch.randint(0, 1 << 20, (E * A,), dtype=torch.int32, device=dev)
     pkg = torch.randint(0, 1 << 30, (E * P,), dtype=torch.int64, device=dev)
@@ -20,6 +20,11 @@ for E in (1024, 2048, 4096, 8192, 16384):
     calls = {
         "empty": lambda: L.exp_empty(E, C.c_void_p(s.cuda_stream)),
         "rt1": lambda: L.exp_rt1(C.c_void_p(rob.data_ptr()), C.c_void_p(pkg.data_ptr()), C.c_void_p(ro.data_ptr()), E, A, P, C.c_void_p(s.cuda_stream)),
+        "rt1_big": lambda: L.exp_rt1_big(C.c_void_p(rob.data_ptr()), C.c_void_p(pkg.data_ptr()), C.c_void_p(ro.data_ptr()), E, A, P, C.c_void_p(s.cuda_stream)),
+        "icache_line": lambda: L.exp_icache(0, C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
+        "icache_loop": lambda: L.exp_icache(1, C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
+        "salu2048": lambda: L.exp_salu(0, C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
+        "mixed1024x2": lambda: L.exp_salu(1, C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
         "rt2": lambda: L.exp_rt2(C.c_void_p(rob.data_ptr()), C.c_void_p(pkg.data_ptr()), C.c_void_p(tab.data_ptr()), C.c_void_p(ro.data_ptr()), E, A, P, C.c_void_p(s.cuda_stream)),
     }
     for name, fn in calls.items():

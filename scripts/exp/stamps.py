@@ -14,27 +14,28 @@ import marl_gpu  # noqa: E402
 from marl_gpu import _lib  # noqa: E402
 from marl_gpu.maps import grid_array, load_map, map_path  # noqa: E402
 
-names = ["loads", "move", "pkgs", "term", "shaping", "tracker", "write"]
+names = ["kernarg", "w_map", "loads_decode", "move", "pkgs", "term", "shape_pre", "agent_loops", "shape_sum",
+         "tracker", "write"]
 res = {}
 for E in [int(x) for x in (sys.argv[1:] or ["1024", "4096"])]:
     env = marl_gpu.BatchedEnv(grid_array(load_map(map_path("map1.txt"))), E, 5, 50, 500, seed=42, tracker="mappo")
     env.reset()
     g = torch.Generator(device="cuda").manual_seed(1)
     acts = torch.randint(0, 15, (300, E, 5), dtype=torch.uint8, device="cuda", generator=g)
-    for k in range(300):
-        env.step(acts[k])
+    if os.environ.get("FUSED"):
+        env.step_fused(acts[:250])
+        env.step_fused(acts[250:])   # stamps of steps 2..8 = the last fused step
+    else:
+        for k in range(300):
+            env.step(acts[k])
     torch.cuda.synchronize()
     buf = np.zeros((65536, 16), np.uint64)
     assert _lib.lib().mdl_debug_stamps(C.c_void_p(buf.ctypes.data), C.c_size_t(buf.nbytes)) == 0
-    st = buf[:E, :8].astype(np.int64)
+    st = buf[:E, :12].astype(np.int64)
     d = np.diff(st, axis=1)
-    t0 = st[:, 0].min()
     res[E] = {
         "median_cycles": {n: float(np.median(d[:, i])) for i, n in enumerate(names)},
-        "mean_cycles": {n: round(float(np.mean(d[:, i])), 1) for i, n in enumerate(names)},
         "p90_cycles": {n: float(np.percentile(d[:, i], 90)) for i, n in enumerate(names)},
-        "wave_total_median": float(np.median(st[:, 7] - st[:, 0])),
-        "start_spread": float(np.percentile(st[:, 0] - t0, 90)),
-        "end_max_minus_first_start": float(st[:, 7].max() - t0),
+        "wave_total_median": float(np.median(st[:, 11] - st[:, 0])),
     }
 print(json.dumps(res, indent=1))

@@ -98,6 +98,23 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
 int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
                    int32_t k_steps, int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
 
+/* ---- rollout glue: keeps MAPPO/trainer.py:133-290 on the device ---- */
+
+/* Categorical(logits=...).sample() and .log_prob() (MAPPO/trainer.py:141-143) for n_rows rows of
+ * n_actions float32 logits (row-major, contiguous).  Inverse CDF of softmax(logits) on a
+ * Philox4x32-10 uniform keyed by (seed, offset, row): deterministic for a given (seed, offset),
+ * independent of launch shape; a caller advances `offset` once per call.  actions: uint8 [n_rows]
+ * (the trainer-int action, ready for mdl_step); log_probs: float32 [n_rows] or NULL. */
+int mdl_sample_actions(const float* logits, int64_t n_rows, int32_t n_actions, uint64_t seed, uint64_t offset,
+                       uint8_t* actions, float* log_probs, void* stream);
+
+/* Generalised advantage estimation exactly as MAPPO/trainer.py:266-276 computes it in float32
+ * (same operation order): rewards, values, dones [T][n] (dones uint8), next_value [n];
+ * gamma = float32(GAMMA), gamma_lambda = float32(GAMMA * GAE_LAMBDA) with the product in double.
+ * Writes advantages and returns (= advantages + values) [T][n]. */
+int mdl_gae(const float* rewards, const float* values, const float* next_value, const uint8_t* dones, int32_t T,
+            int64_t n, float gamma, float gamma_lambda, float* advantages, float* returns, void* stream);
+
 /* Observation builders for envs [env_begin, env_begin+n), which must share one
  * map shape (H, W), from the current state + tracker:
  *   actor_map  f32 [n][A][6][H][W]          convert_observation       MAPPO/helper.py:6-66

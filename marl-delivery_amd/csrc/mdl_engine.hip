@@ -17,8 +17,13 @@
 #include "mdl_kernels.hpp"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
+
+// the library-wide error slot behind mdl_last_error() (mdl_kernels.hpp)
+void mdl::set_error(const char* msg) { g_err = msg; }
+
+namespace {
 
 int fail(const char* fmt, ...) {
     char buf[512];

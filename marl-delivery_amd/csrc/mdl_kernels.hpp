@@ -4,6 +4,9 @@
 
 namespace mdl {
 
+// sets the thread-local message mdl_last_error() returns (mdl_engine.hip)
+void set_error(const char* msg);
+
 struct ShapingConsts {
     float c[9];
 };

@@ -98,6 +98,16 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
 int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
                    int32_t k_steps, int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
 
+/* ---- checkpoint of the engine state ----
+ * A versioned host blob: a 56-byte header (magic "MDLSTATE", version, E, A, P, T, tracker mode,
+ * map fingerprint) then every state buffer (robots, packages, state words, env records,
+ * MT19937 states, tracker data, episode results).  Loading it into an engine of the same
+ * configuration resumes every env's stream exactly, RNG included; any other engine refuses it.
+ * save / load are synchronous on `stream`; the buffer is host memory. */
+int mdl_state_bytes(MdlEngine* eng, int64_t* bytes);
+int mdl_save_state(MdlEngine* eng, void* host_buf, int64_t bytes, void* stream);
+int mdl_load_state(MdlEngine* eng, const void* host_buf, int64_t bytes, void* stream);
+
 /* ---- rollout glue: keeps MAPPO/trainer.py:133-290 on the device ---- */
 
 /* Categorical(logits=...).sample() and .log_prob() (MAPPO/trainer.py:141-143) for n_rows rows of

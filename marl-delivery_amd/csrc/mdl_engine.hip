@@ -102,6 +102,15 @@ struct MdlEngine {
     int wpb_step = 1, wpb_obs = 1;
     int maxHW = 0;
     bool seeded = false;
+    uint64_t map_fp = 0;  // FNV-1a of every map's (H, W, cells, env_map): checkpoint compatibility
+
+    // (device pointer, bytes) of every state buffer, in checkpoint order
+    std::vector<std::pair<void*, size_t>> state_sections() const {
+        const size_t E = p.E, A = p.A, P = p.P;
+        return {{p.rob, E * A * 4},   {p.pkg, E * P * 8},     {p.pstate, E * P * 2},
+                {p.es, E * 16},       {p.mt, E * mdl::MT_N * 4}, {p.mt_pos, E * 4},
+                {p.trk, p.stale ? E * P * 8 : 0}, {p.ep_total, E * 8}, {p.ep_len, E * 4}};
+    }
 
     template <class T>
     int alloc(T** ptr, size_t count) {
@@ -292,6 +301,19 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     p.free_cells = d_free;
     p.rank = d_rank;
     p.env_map = d_em;
+    {
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&h](uint64_t v) {
+            for (int b = 0; b < 8; b++) {
+                h ^= (v >> (8 * b)) & 0xff;
+                h *= 1099511628211ull;
+            }
+        };
+        for (int m = 0; m < n_maps; m++) mix(((uint64_t)eng->mapH[m] << 32) | (uint32_t)eng->mapW[m]);
+        for (uint8_t v : allgrid) mix(v);
+        for (uint8_t v : em) mix(v);
+        eng->map_fp = h;
+    }
 
     eng->lds_step = mdl::step_lds((int)P);
     eng->wpb_step = waves_per_block(eng->lds_step);
@@ -379,6 +401,76 @@ int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format
     DeviceGuard dg(eng->device);
     HIPCHK(mdl::launch_step_fused(eng->p, actions, action_format, env_ids, n, k_steps, auto_reset, r_env, r_shaped,
                                   done, eng->wpb_step, eng->lds_step, (hipStream_t)stream));
+    return 0;
+}
+
+// ---- checkpoint ----
+namespace {
+struct CkptHeader {
+    char magic[8];  // "MDLSTATE"
+    uint32_t version, tracker_mode;
+    int32_t E, A, P, T, n_maps, seeded;
+    uint64_t map_fp, payload_bytes;
+};
+static_assert(sizeof(CkptHeader) == 56, "checkpoint header layout");
+}  // namespace
+
+int mdl_state_bytes(MdlEngine* eng, int64_t* bytes) {
+    if (!eng || !bytes) return fail("mdl_state_bytes: null argument");
+    size_t n = sizeof(CkptHeader);
+    for (auto& s : eng->state_sections()) n += s.second;
+    *bytes = (int64_t)n;
+    return 0;
+}
+
+int mdl_save_state(MdlEngine* eng, void* buf, int64_t bytes, void* stream) {
+    int64_t need = 0;
+    if (mdl_state_bytes(eng, &need)) return -1;
+    if (!buf || bytes < need) return fail("mdl_save_state: buffer of %lld bytes, need %lld", (long long)bytes,
+                                          (long long)need);
+    DeviceGuard dg(eng->device);
+    hipStream_t s = (hipStream_t)stream;
+    CkptHeader h{};
+    memcpy(h.magic, "MDLSTATE", 8);
+    h.version = 1;
+    h.tracker_mode = (uint32_t)eng->cfg.tracker_mode;
+    h.E = eng->p.E; h.A = eng->p.A; h.P = eng->p.P; h.T = eng->p.T;
+    h.n_maps = eng->p.n_maps;
+    h.seeded = eng->seeded ? 1 : 0;
+    h.map_fp = eng->map_fp;
+    h.payload_bytes = (uint64_t)(need - (int64_t)sizeof(CkptHeader));
+    memcpy(buf, &h, sizeof h);
+    char* o = (char*)buf + sizeof h;
+    for (auto& sec : eng->state_sections()) {
+        if (sec.second) HIPCHK(hipMemcpyAsync(o, sec.first, sec.second, hipMemcpyDeviceToHost, s));
+        o += sec.second;
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int mdl_load_state(MdlEngine* eng, const void* buf, int64_t bytes, void* stream) {
+    int64_t need = 0;
+    if (mdl_state_bytes(eng, &need)) return -1;
+    if (!buf || bytes < (int64_t)sizeof(CkptHeader)) return fail("mdl_load_state: truncated checkpoint");
+    CkptHeader h;
+    memcpy(&h, buf, sizeof h);
+    if (memcmp(h.magic, "MDLSTATE", 8) != 0 || h.version != 1) return fail("mdl_load_state: not an engine checkpoint");
+    if (h.E != eng->p.E || h.A != eng->p.A || h.P != eng->p.P || h.T != eng->p.T ||
+        h.tracker_mode != (uint32_t)eng->cfg.tracker_mode || h.n_maps != eng->p.n_maps || h.map_fp != eng->map_fp)
+        return fail("mdl_load_state: checkpoint of a different configuration (E=%d A=%d P=%d T=%d, maps %llx)", h.E, h.A,
+                    h.P, h.T, (unsigned long long)h.map_fp);
+    if (bytes < need || h.payload_bytes != (uint64_t)(need - (int64_t)sizeof h))
+        return fail("mdl_load_state: checkpoint of %lld bytes, need %lld", (long long)bytes, (long long)need);
+    DeviceGuard dg(eng->device);
+    hipStream_t s = (hipStream_t)stream;
+    const char* in = (const char*)buf + sizeof h;
+    for (auto& sec : eng->state_sections()) {
+        if (sec.second) HIPCHK(hipMemcpyAsync(sec.first, in, sec.second, hipMemcpyHostToDevice, s));
+        in += sec.second;
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    eng->seeded = h.seeded != 0;
     return 0;
 }
 

@@ -221,6 +221,26 @@ class BatchedEnv:
                                   ptr(p["critic_map"]), ptr(p["critic_vec"]), self._stream()), "mdl_build_obs")
         return out
 
+    # ---- checkpoint: engine state incl. every env's MT19937 stream ----
+    def save_state(self, path=None) -> np.ndarray:
+        """Snapshot of the whole engine state as a uint8 array (written to ``path`` as .npy
+        when given).  Loading it into an engine built with the same configuration resumes
+        every env exactly (the reference cannot: its RandomState lives inside each env)."""
+        n = C.c_int64()
+        check(lib().mdl_state_bytes(self._h, C.byref(n)), "mdl_state_bytes")
+        buf = np.zeros(n.value, np.uint8)
+        check(lib().mdl_save_state(self._h, buf.ctypes.data, n.value, self._stream()), "mdl_save_state")
+        if path is not None:
+            np.save(path, buf, allow_pickle=False)
+        return buf
+
+    def load_state(self, src) -> None:
+        """Restore a ``save_state`` snapshot (array or .npy path); raises on a mismatched engine."""
+        buf = np.load(src, allow_pickle=False) if isinstance(src, (str, bytes)) or hasattr(src, "__fspath__") \
+            else np.asarray(src)
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        check(lib().mdl_load_state(self._h, buf.ctypes.data, buf.nbytes, self._stream()), "mdl_load_state")
+
     def read_state(self):
         """int32/f64 device tensors: robots [E,A,3] (r,c,carry), pkgs [E,P,8]
         (sr,sc,tr,tc,start_time,deadline,id,status), t [E], total_reward [E],

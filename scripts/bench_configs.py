@@ -94,6 +94,40 @@ def run(cfg, steps, warmup):
     env.close()
 
 
+def run_rollout(steps):
+    """MAPPO rollout on the device: 4096 envs, map1, A=5, the
+    trainer's featurizer sizes, a linear actor on the 52-dim vector and a linear
+    critic on the 1301-dim vector; sampling, step, obs into the buffers and GAE
+    all on the device.  Reports env agent-steps/s of whole rollouts."""
+    import marl_gpu
+    import marl_gpu.rollout as R
+    from marl_gpu.maps import grid_array, load_map, map_path
+    E, A, P, T = 4096, 5, 50, 500
+    env = marl_gpu.BatchedEnv(grid_array(load_map(map_path("map1.txt"))), E, A, P, T, seed=42, tracker="mappo",
+                              max_other_robots=A - 1, max_packages_obs=5)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    wa = torch.randn(env.actor_vec_dim, 15, device="cuda", generator=g) * 0.1
+    wc = torch.randn(env.critic_vec_dim, device="cuda", generator=g) * 0.01
+    actor = lambda obs, vec: vec @ wa  # noqa: E731
+    critic = lambda gmap, gvec: gvec @ wc  # noqa: E731
+    Tr = 128
+    ro = R.MappoRollout(env, Tr, seed=1)
+    ro.collect(actor, critic)
+    torch.cuda.synchronize()
+    n = max(1, steps // Tr)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        ro.collect(actor, critic)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"config": "rollout", "envs": E, "agents": A, "rollout_steps": Tr, "rollouts": n,
+           "us_per_env_step": dt / (n * Tr) * 1e6, "agent_steps_per_s": E * A * n * Tr / dt,
+           "note": "MappoRollout.collect: linear actor/critic (torch), on-device sampling, mdl_step, mdl_build_obs "
+                   "into the rollout buffers, GAE kernel"}
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="3,3b,4,5")
@@ -102,7 +136,10 @@ def main():
     a = ap.parse_args()
     torch.cuda.set_device(0)
     for c in a.config.split(","):
-        run(c, a.steps, a.warmup)
+        if c == "rollout":
+            run_rollout(a.steps)
+        else:
+            run(c, a.steps, a.warmup)
 
 
 if __name__ == "__main__":

@@ -98,6 +98,16 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
 int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
                    int32_t k_steps, int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
 
+/* ---- greedy baseline: greedyagent.py batched on the device ----
+ * mdl_greedy_init = GreedyAgents() + init_agents(state) for the listed envs (call it right
+ * after their reset, as evaluation.py:29-35 does); the first call also builds run_bfs's
+ * distance field for every cell of every map (maps of <= 4096 cells).
+ * mdl_greedy_actions = one get_actions(state) per listed env (call once per step, before
+ * mdl_step), written as MDL_ACTION_CODES bytes [n][A].  Bug-compatible with the reference
+ * agent (duplicated t=0 package entries, id-1 list indexing). */
+int mdl_greedy_init(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream);
+int mdl_greedy_actions(MdlEngine* eng, const int32_t* env_ids, int32_t n, uint8_t* actions, void* stream);
+
 /* ---- checkpoint of the engine state ----
  * A versioned host blob: a 56-byte header (magic "MDLSTATE", version, E, A, P, T, tracker mode,
  * map fingerprint) then every state buffer (robots, packages, state words, env records,

@@ -103,6 +103,10 @@ struct MdlEngine {
     int maxHW = 0;
     bool seeded = false;
     uint64_t map_fp = 0;  // FNV-1a of every map's (H, W, cells, env_map): checkpoint compatibility
+    // greedy baseline (mdl_greedy_*): BFS tables per map and one agent record per env, made on first use
+    uint16_t* gtab = nullptr;
+    unsigned char* gstate = nullptr;
+    mdl::GreedyLayout glay{};
 
     // (device pointer, bytes) of every state buffer, in checkpoint order
     std::vector<std::pair<void*, size_t>> state_sections() const {
@@ -401,6 +405,53 @@ int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format
     DeviceGuard dg(eng->device);
     HIPCHK(mdl::launch_step_fused(eng->p, actions, action_format, env_ids, n, k_steps, auto_reset, r_env, r_shaped,
                                   done, eng->wpb_step, eng->lds_step, (hipStream_t)stream));
+    return 0;
+}
+
+// ---- greedy baseline ----
+int mdl_greedy_init(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream) {
+    if (!eng) return fail("mdl_greedy_init: null engine");
+    if (!eng->seeded) return fail("mdl_greedy_init: engine not seeded");
+    if (!env_ids) n = eng->p.E;
+    if (n < 0 || n > eng->p.E) return fail("mdl_greedy_init: n=%d out of range", n);
+    DeviceGuard dg(eng->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (!eng->gtab) {
+        mdl::GreedyLayout& g = eng->glay;
+        g.A = eng->p.A;
+        g.cap = 3 * eng->p.P + 64;
+        g.list_off = (8 + 4 * g.A + 3) & ~3;
+        g.free_off = g.list_off + 2 * g.cap;
+        g.stride = (g.free_off + g.cap + 15) & ~15;
+        g.lds_stride = (3 * g.cap + 15) & ~15;
+        if (4 * (size_t)g.lds_stride > LDS_BUDGET) return fail("mdl_greedy_init: too many packages for the greedy agent");
+        int64_t tab = 0;
+        for (int m = 0; m < eng->p.n_maps; m++) {
+            const int64_t hw = (int64_t)eng->mapH[m] * eng->mapW[m];
+            if (hw > 4096) return fail("mdl_greedy_init: map %d has %lld cells (the BFS tables need <= 4096)", m,
+                                       (long long)hw);
+            g.tab_off[m] = tab;
+            tab += hw * hw;
+        }
+        if (eng->alloc(&eng->gtab, (size_t)tab) || eng->alloc(&eng->gstate, (size_t)eng->p.E * g.stride)) return -1;
+        for (int m = 0; m < eng->p.n_maps; m++)
+            HIPCHK(mdl::launch_bfs_table(eng->p.grids + eng->p.maps[m].grid_off, eng->mapH[m], eng->mapW[m],
+                                         eng->gtab + g.tab_off[m], s));
+    }
+    if (n == 0) return 0;
+    HIPCHK(mdl::launch_greedy_init(eng->p, eng->glay, eng->gstate, env_ids, n, s));
+    return 0;
+}
+
+int mdl_greedy_actions(MdlEngine* eng, const int32_t* env_ids, int32_t n, uint8_t* actions, void* stream) {
+    if (!eng || !actions) return fail("mdl_greedy_actions: null argument");
+    if (!eng->gstate) return fail("mdl_greedy_actions: call mdl_greedy_init first");
+    if (!env_ids) n = eng->p.E;
+    if (n < 0 || n > eng->p.E) return fail("mdl_greedy_actions: n=%d out of range", n);
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_greedy_act(eng->p, eng->glay, eng->gstate, eng->gtab, env_ids, n, actions,
+                                  (hipStream_t)stream));
     return 0;
 }
 

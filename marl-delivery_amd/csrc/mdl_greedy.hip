@@ -1,0 +1,264 @@
+// mdl_greedy.hip -- the reference's greedy baseline (greedyagent.py) batched on
+// the device, so the README evaluation row runs at scale.
+//
+//   k_bfs_table    run_bfs's distance field (greedyagent.py:6-29) for every goal
+//                  cell of a map: one workgroup per goal, level-synchronous BFS in
+//                  LDS; table[goal][cell] u16 (0xffff = not reached)
+//   k_greedy_init  GreedyAgents() + init_agents(state)      greedyagent.py:44-64
+//   k_greedy_act   get_actions(state) -> action codes       greedyagent.py:104-170
+//
+// The agent is restated bug for bug (the test suite checks it action for action):
+// the package list holds each t=0 spawn twice (init_agents and the first
+// get_actions both append it) and is indexed by id-1 for packages_free and
+// packages[...], so targets can point at another package's cells.  One wave per
+// env; the robots' target choice is sequential (packages_free is shared), the
+// BFS lookups then run on the robot lanes.
+#include "mdl_kernels.hpp"
+
+namespace mdl {
+
+constexpr uint16_t BFS_INF = 0xffff;
+
+__global__ __launch_bounds__(256) void k_bfs_table(const uint8_t* __restrict__ grid, int H, int W,
+                                                   uint16_t* __restrict__ table) {
+    extern __shared__ uint16_t d[];
+    __shared__ int changed;
+    const int HW = H * W;
+    const int goal = blockIdx.x;
+    for (int i = threadIdx.x; i < HW; i += blockDim.x) d[i] = i == goal ? 0 : BFS_INF;
+    __syncthreads();
+    for (int level = 0;; level++) {
+        if (threadIdx.x == 0) changed = 0;
+        __syncthreads();
+        int ch = 0;
+        for (int i = threadIdx.x; i < HW; i += blockDim.x) {
+            if (d[i] != level) continue;
+            const int r = i / W, c = i - (i / W) * W;
+            // neighbours in bounds, free, not yet reached (greedyagent.py:18-24)
+            if (r > 0 && grid[i - W] == 0 && d[i - W] == BFS_INF) { d[i - W] = (uint16_t)(level + 1); ch = 1; }
+            if (r + 1 < H && grid[i + W] == 0 && d[i + W] == BFS_INF) { d[i + W] = (uint16_t)(level + 1); ch = 1; }
+            if (c > 0 && grid[i - 1] == 0 && d[i - 1] == BFS_INF) { d[i - 1] = (uint16_t)(level + 1); ch = 1; }
+            if (c + 1 < W && grid[i + 1] == 0 && d[i + 1] == BFS_INF) { d[i + 1] = (uint16_t)(level + 1); ch = 1; }
+        }
+        if (ch) changed = 1;  // benign race: every writer stores 1
+        __syncthreads();
+        const int any = changed;
+        __syncthreads();
+        if (!any) break;
+    }
+    uint16_t* row = table + (size_t)goal * HW;
+    for (int i = threadIdx.x; i < HW; i += blockDim.x) row[i] = d[i];
+}
+
+// Per-env agent record (GreedyLayout): n, flags | target[A] i16 | prev_carry[A] i16 |
+// list[cap] u16 (package ids in append order) | free[cap] u8
+struct GreedyRec {
+    int32_t* n;
+    int32_t* flags;  // bit 0: list overflow
+    int16_t* target;
+    int16_t* prev_carry;
+    uint16_t* list;
+    uint8_t* free_;
+};
+
+__device__ inline GreedyRec greedy_rec(unsigned char* base, const GreedyLayout& g, int e) {
+    unsigned char* b = base + (size_t)e * g.stride;
+    GreedyRec r;
+    r.n = (int32_t*)b;
+    r.flags = (int32_t*)(b + 4);
+    r.target = (int16_t*)(b + 8);
+    r.prev_carry = (int16_t*)(b + 8 + 2 * g.A);
+    r.list = (uint16_t*)(b + g.list_off);
+    r.free_ = b + g.free_off;
+    return r;
+}
+
+// state['packages'] at this t: append the spawns (start_time == t) in id order
+__device__ inline void greedy_append(const DevParams& p, const GreedyLayout& g, GreedyRec& R, int e, int t) {
+    const int lane = lane_id();
+    int n = *R.n;
+    for (int j0 = 0; j0 < p.P; j0 += WAVE) {
+        const int j = j0 + lane;
+        const bool sp = j < p.P && pk_st(p.pkg[(size_t)e * p.P + j]) == t;
+        const uint64_t b = ballot(sp);
+        const int pos = n + popc64(b & lanemask_lt());
+        if (sp && pos < g.cap) {
+            R.list[pos] = (uint16_t)(j + 1);
+            R.free_[pos] = 1;
+        }
+        n += popc64(b);
+    }
+    if (lane == 0) {
+        if (n > g.cap) *R.flags |= 1;
+        *R.n = n < g.cap ? n : g.cap;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_greedy_init(DevParams p, GreedyLayout g, unsigned char* __restrict__ gs,
+                                                     const int* __restrict__ env_ids, int n) {
+    const int w = blockIdx.x * 4 + wave_id();
+    if (w >= n) return;
+    const int e = env_ids ? env_ids[w] : w;
+    const int lane = lane_id();
+    GreedyRec R = greedy_rec(gs, g, e);
+    if (lane < p.A) {
+        R.target[lane] = 0;
+        R.prev_carry[lane] = 0;   // init_agents stores carrying = 0
+    }
+    if (lane == 0) {
+        *R.n = 0;
+        *R.flags = 0;
+    }
+    wave_sync();
+    greedy_append(p, g, R, e, p.es[e].t);
+}
+
+// One get_actions(state) per env; actions[w][a] = move code | op << 3 (MDL_ACTION_CODES).
+// The env's list and free flags are staged in its wave's LDS slice (list u16[cap], free u8[cap]).
+__global__ __launch_bounds__(256) void k_greedy_act(DevParams p, GreedyLayout g, unsigned char* __restrict__ gs,
+                                                    const uint16_t* __restrict__ tables, const int* __restrict__ env_ids,
+                                                    int n, uint8_t* __restrict__ actions) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int wave = wave_id();
+    const int w = blockIdx.x * 4 + wave;
+    if (w >= n) return;
+    const int e = env_ids ? env_ids[w] : w;
+    const int lane = lane_id();
+    const int A = p.A, P = p.P, cap = g.cap;
+    uint16_t* list = (uint16_t*)(smem + (size_t)wave * g.lds_stride);
+    uint8_t* free_ = (uint8_t*)(list + cap);
+    const int mi = p.env_map ? p.env_map[e] : 0;
+    const MapDesc md = p.maps[mi];
+    const int H = md.H, W = md.W, HW = H * W;
+    GreedyRec R = greedy_rec(gs, g, e);
+    const int t = p.es[e].t;
+    const uint64_t* pk = p.pkg + (size_t)e * P;
+    // update_inner_state (greedyagent.py:104-125): robots, targets of robots that were carrying
+    const bool act = lane < A;
+    const uint32_t rv = act ? p.rob[(size_t)e * A + lane] : 0u;
+    const int cell = rob_cell(rv), carry = rob_carry(rv);
+    int target = act ? R.target[lane] : 0;
+    if (act && R.prev_carry[lane] != 0) target = carry == 0 ? 0 : carry;
+    int nl = *R.n;
+    for (int j = lane; j < nl; j += WAVE) {
+        list[j] = R.list[j];
+        free_[j] = R.free_[j];
+    }
+    // ... and the packages of this state (spawns at t), appended in id order
+    int flags = 0;
+    for (int j0 = 0; j0 < P; j0 += WAVE) {
+        const int j = j0 + lane;
+        const bool sp = j < P && pk_st(pk[j]) == t;
+        const uint64_t b = ballot(sp);
+        const int pos = nl + popc64(b & lanemask_lt());
+        if (sp && pos < cap) {
+            list[pos] = (uint16_t)(j + 1);
+            free_[pos] = 1;
+        }
+        nl += popc64(b);
+    }
+    if (nl > cap) {
+        flags = 1;
+        nl = cap;
+    }
+    wave_sync();
+    // target choice, robot by robot (get_actions greedyagent.py:127-170)
+    int idx = -1, phase = 0;  // this robot lane's list index and 1 = heading to the target cell
+    for (int i = 0; i < A; i++) {
+        const int ti = rdl(target, i);
+        int ii = -1, ph = 0;
+        if (ti != 0) {
+            ii = ti - 1;
+            ph = rdl(carry, i) != 0;
+        } else {
+            // closest free list entry by Manhattan distance to its start; strict < keeps the first
+            const int ci = rdl(cell, i);
+            uint32_t best = 0xffffffffu;
+            for (int j0 = 0; j0 < nl; j0 += WAVE) {
+                const int j = j0 + lane;
+                uint32_t key = 0xffffffffu;
+                if (j < nl && free_[j]) key = ((uint32_t)manhattan(pk_start(pk[list[j] - 1]), ci) << 16) | (uint32_t)j;
+                const uint32_t m = wave_min_u32(key);
+                best = m < best ? m : best;
+            }
+            if (best != 0xffffffffu) {
+                const int closest = list[best & 0xffff];
+                if (lane == 0) free_[closest - 1] = 0;   // packages_free[closest_package_id - 1]
+                wave_sync();
+                ii = closest - 1;
+                if (lane == i) target = closest;
+            }
+        }
+        if (lane == i) {
+            idx = ii;
+            phase = ph;
+        }
+    }
+    // update_move_to_target (greedyagent.py:66-102) on the robot lanes
+    int mv = MV_S, op = 0;
+    if (act && idx >= 0) {
+        const uint64_t d = pk[list[idx] - 1];           // self.packages[target_package_id]
+        const int pt = phase ? pk_target(d) : pk_start(d);
+        const int pr = cell_r(pt), pc = cell_c(pt), rr = cell_r(cell), rc = cell_c(cell);
+        op = phase ? 2 : 1;
+        if (abs(pr - rr) + abs(pc - rc) >= 1) {
+            // run_bfs: distances from the goal; the first neighbour in U, D, L, R order one
+            // step closer, else 'S'; unreachable start -> ('S', 100000)
+            const uint16_t* Dg = tables + g.tab_off[mi] + (size_t)(pr * W + pc) * HW;
+            const int s = rr * W + rc;
+            const int ds = Dg[s];
+            int d2 = 100000;
+            if (ds != BFS_INF) {
+                d2 = ds;
+                const int nb[4] = {rr > 0 ? s - W : -1, rr + 1 < H ? s + W : -1, rc > 0 ? s - 1 : -1,
+                                   rc + 1 < W ? s + 1 : -1};
+                const int code[4] = {MV_U, MV_D, MV_L, MV_R};
+#pragma unroll
+                for (int k = 3; k >= 0; k--) {
+                    if (nb[k] >= 0) {
+                        const int dn = Dg[nb[k]];
+                        if (dn != BFS_INF && dn == ds - 1) {
+                            mv = code[k];
+                            d2 = dn;
+                        }
+                    }
+                }
+            }
+            if (d2 != 0) op = 0;
+        }
+    }
+    // write back the agent record
+    if (act) {
+        R.target[lane] = (int16_t)target;
+        R.prev_carry[lane] = (int16_t)carry;
+        actions[(size_t)w * A + lane] = (uint8_t)(mv | (op << 3));
+    }
+    for (int j = lane; j < nl; j += WAVE) {
+        R.list[j] = list[j];
+        R.free_[j] = free_[j];
+    }
+    if (lane == 0) {
+        *R.n = nl;
+        *R.flags |= flags;
+    }
+}
+
+hipError_t launch_bfs_table(const uint8_t* grid, int H, int W, uint16_t* table, hipStream_t s) {
+    hipLaunchKernelGGL(k_bfs_table, dim3(H * W), dim3(256), (size_t)H * W * 2, s, grid, H, W, table);
+    return hipGetLastError();
+}
+
+hipError_t launch_greedy_init(const DevParams& p, const GreedyLayout& g, unsigned char* gs, const int* ids, int n,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_greedy_init, dim3((n + 3) / 4), dim3(256), 0, s, p, g, gs, ids, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_greedy_act(const DevParams& p, const GreedyLayout& g, unsigned char* gs, const uint16_t* tables,
+                             const int* ids, int n, uint8_t* actions, hipStream_t s) {
+    hipLaunchKernelGGL(k_greedy_act, dim3((n + 3) / 4), dim3(256), 4 * (size_t)g.lds_stride, s, p, g, gs, tables, ids,
+                       n, actions);
+    return hipGetLastError();
+}
+
+}  // namespace mdl

@@ -32,6 +32,17 @@ hipError_t launch_views_shaped(const DevParams& p, const int32_t* prev, const in
 hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int32_t* t, double* total,
                          int32_t* tracker, int32_t* tracker_data, hipStream_t s);
 
+// Greedy agent record layout (mdl_greedy.hip): per env `stride` bytes.
+struct GreedyLayout {
+    int A, cap, stride, list_off, free_off, lds_stride;
+    int64_t tab_off[MAX_MAPS];  // BFS table of map m: tables + tab_off[m], [HW goal][HW cell] u16
+};
+hipError_t launch_bfs_table(const uint8_t* grid, int H, int W, uint16_t* table, hipStream_t s);
+hipError_t launch_greedy_init(const DevParams& p, const GreedyLayout& g, unsigned char* gs, const int* ids, int n,
+                              hipStream_t s);
+hipError_t launch_greedy_act(const DevParams& p, const GreedyLayout& g, unsigned char* gs, const uint16_t* tables,
+                             const int* ids, int n, uint8_t* actions, hipStream_t s);
+
 size_t step_lds(int P);
 size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs);
 size_t views_lds(int NSmax, int HW, int MO, int MPc, int MR, int MPsc);

@@ -56,6 +56,8 @@ SIGNATURES = {
     "mdl_step": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mdl_step_fused": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mdl_build_obs": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "mdl_greedy_init": (C.c_int, [_vp, _vp, _i32, _vp]),
+    "mdl_greedy_actions": (C.c_int, [_vp, _vp, _i32, _vp, _vp]),
     "mdl_state_bytes": (C.c_int, [_vp, C.POINTER(C.c_int64)]),
     "mdl_save_state": (C.c_int, [_vp, _vp, C.c_int64, _vp]),
     "mdl_load_state": (C.c_int, [_vp, _vp, C.c_int64, _vp]),

@@ -221,6 +221,22 @@ class BatchedEnv:
                                   ptr(p["critic_map"]), ptr(p["critic_vec"]), self._stream()), "mdl_build_obs")
         return out
 
+    # ---- greedy baseline: greedyagent.py batched on the device ----
+    def greedy_init(self, env_ids=None):
+        """``GreedyAgents()`` + ``init_agents(state)`` for the listed envs (right after their reset)."""
+        ids, n = self._ids(env_ids)
+        check(lib().mdl_greedy_init(self._h, ptr(ids), n, self._stream()), "mdl_greedy_init")
+        self._keep_g = ids
+
+    def greedy_actions(self, env_ids=None, out=None) -> torch.Tensor:
+        """One ``get_actions(state)`` per listed env: uint8 [n, A] in the "codes" action format."""
+        ids, n = self._ids(env_ids)
+        if out is None:
+            out = torch.empty((n, self.A), dtype=torch.uint8, device=self.device)
+        check(lib().mdl_greedy_actions(self._h, ptr(ids), n, ptr(out), self._stream()), "mdl_greedy_actions")
+        self._keep_g = ids
+        return out
+
     # ---- checkpoint (SURVEY.md §8(f)4): engine state incl. every env's MT19937 stream ----
     def save_state(self, path=None) -> np.ndarray:
         """Snapshot of the whole engine state as a uint8 array (written to ``path`` as .npy

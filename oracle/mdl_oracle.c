@@ -794,3 +794,144 @@ void or_batch_step(OBatch* b, const uint8_t* actions_int, int auto_reset, const 
         if (opp != op) free(opp);
     }
 }
+
+/* ----------------------------------------------------------------------- */
+/* GreedyAgents (greedyagent.py), literal: BFS from the goal on every call, */
+/* the package list exactly as the agent builds it (init_agents and the     */
+/* first get_actions both append the t=0 spawns, so they appear twice, and  */
+/* packages[id-1] / packages_free[id-1] index that list by id).             */
+/* ----------------------------------------------------------------------- */
+typedef struct {
+    int A, P, n, is_init;
+    int* list;          /* package ids in append order (greedyagent.py:60,135) */
+    uint8_t* free_;     /* packages_free */
+    int* target;        /* robots_target: 0 = 'free', else package id */
+    ORobot* robots;     /* inner robots (0-indexed r, c, carrying) */
+    int* bd;            /* BFS scratch: distances, queue */
+    int* bq;
+} OGreedy;
+
+OGreedy* or_greedy_new(int A, int P, int H, int W) {
+    OGreedy* g = (OGreedy*)calloc(1, sizeof(OGreedy));
+    g->A = A; g->P = P;
+    g->list = (int*)calloc((size_t)(2 * P + 1), sizeof(int));
+    g->free_ = (uint8_t*)calloc((size_t)(2 * P + 1), 1);
+    g->target = (int*)calloc((size_t)(A + 1), sizeof(int));
+    g->robots = (ORobot*)calloc((size_t)(A + 1), sizeof(ORobot));
+    g->bd = (int*)malloc(sizeof(int) * (size_t)H * W);
+    g->bq = (int*)malloc(sizeof(int) * (size_t)H * W);
+    return g;
+}
+
+void or_greedy_free(OGreedy* g) {
+    if (!g) return;
+    free(g->list); free(g->free_); free(g->target); free(g->robots); free(g->bd); free(g->bq); free(g);
+}
+
+/* state['packages'] = this step's spawns (env.py:133-137), appended in id order */
+static void greedy_append(OGreedy* g, const OEnv* e) {
+    for (int i = 0; i < e->P; i++)
+        if (e->pkgs[i].start_time == e->t) {
+            g->list[g->n] = e->pkgs[i].id;
+            g->free_[g->n] = 1;
+            g->n++;
+        }
+}
+
+/* greedyagent.py:54-64 init_agents */
+void or_greedy_init(OGreedy* g, const OEnv* e) {
+    g->n = 0;
+    g->is_init = 0;
+    for (int i = 0; i < g->A; i++) {
+        g->robots[i].r = e->robots[i].r;
+        g->robots[i].c = e->robots[i].c;
+        g->robots[i].carrying = 0;
+        g->target[i] = 0;
+    }
+    greedy_append(g, e);
+}
+
+/* greedyagent.py:6-41 run_bfs(map, start, goal): returns the move, *dist = d after the move */
+static int greedy_bfs(OGreedy* g, const OEnv* e, int sr, int sc, int gr, int gc, int* dist) {
+    const int H = e->H, W = e->W;
+    for (int i = 0; i < H * W; i++) g->bd[i] = -1;
+    int qh = 0, qt = 0;
+    g->bd[gr * W + gc] = 0;
+    g->bq[qt++] = gr * W + gc;
+    static const int DR[4] = {-1, 1, 0, 0}, DC[4] = {0, 0, -1, 1};
+    while (qh < qt) {
+        int cur = g->bq[qh++];
+        int r = cur / W, c = cur % W;
+        for (int k = 0; k < 4; k++) {
+            int nr = r + DR[k], nc = c + DC[k];
+            if (nr < 0 || nr >= H || nc < 0 || nc >= W) continue;
+            if (g->bd[nr * W + nc] < 0 && e->grid[nr * W + nc] == 0) {
+                g->bd[nr * W + nc] = g->bd[cur] + 1;
+                g->bq[qt++] = nr * W + nc;
+            }
+        }
+    }
+    int ds = g->bd[sr * W + sc];
+    if (ds < 0) { *dist = 100000; return MV_S; }
+    static const int MOVES[4] = {MV_U, MV_D, MV_L, MV_R};   /* actions = ['U','D','L','R'] */
+    for (int k = 0; k < 4; k++) {
+        int nr = sr + DR[k], nc = sc + DC[k];
+        if (nr < 0 || nr >= H || nc < 0 || nc >= W) continue;
+        int dn = g->bd[nr * W + nc];
+        if (dn >= 0 && dn == ds - 1) { *dist = dn; return MOVES[k]; }
+    }
+    *dist = ds;
+    return MV_S;
+}
+
+/* greedyagent.py:66-102 update_move_to_target(robot, target_package_id = list index, phase) */
+static void greedy_move_to(OGreedy* g, const OEnv* e, int i, int idx, int phase_target, uint8_t* mv, uint8_t* op) {
+    const OPkg* p = &e->pkgs[g->list[idx] - 1];   /* self.packages[target_package_id] */
+    int pr = phase_target ? p->tr : p->sr, pc = phase_target ? p->tc : p->sc;
+    int distance = abs(pr - g->robots[i].r) + abs(pc - g->robots[i].c);
+    int pkg_act = 0, move = MV_S;
+    if (distance >= 1) {
+        int d2;
+        move = greedy_bfs(g, e, g->robots[i].r, g->robots[i].c, pr, pc, &d2);
+        if (d2 == 0) pkg_act = phase_target ? 2 : 1;
+    } else {
+        pkg_act = phase_target ? 2 : 1;
+    }
+    mv[i] = (uint8_t)move;
+    op[i] = (uint8_t)pkg_act;
+}
+
+/* greedyagent.py:104-170 update_inner_state + get_actions; mv/op: MV_* codes and 0/1/2 */
+void or_greedy_actions(OGreedy* g, const OEnv* e, uint8_t* mv, uint8_t* op) {
+    g->is_init = 1;
+    for (int i = 0; i < g->A; i++) {                       /* update_inner_state */
+        int prev_carry = g->robots[i].carrying;
+        g->robots[i].r = e->robots[i].r;
+        g->robots[i].c = e->robots[i].c;
+        g->robots[i].carrying = e->robots[i].carrying;
+        if (prev_carry != 0) g->target[i] = e->robots[i].carrying == 0 ? 0 : e->robots[i].carrying;
+    }
+    greedy_append(g, e);
+    for (int i = 0; i < g->A; i++) {
+        if (g->target[i] != 0) {
+            int pid = g->target[i];
+            greedy_move_to(g, e, i, pid - 1, g->robots[i].carrying != 0, mv, op);
+        } else {
+            int closest = 0, best = 1000000;
+            for (int j = 0; j < g->n; j++) {
+                if (!g->free_[j]) continue;
+                const OPkg* p = &e->pkgs[g->list[j] - 1];
+                int d = abs(p->sr - g->robots[i].r) + abs(p->sc - g->robots[i].c);
+                if (d < best) { best = d; closest = g->list[j]; }
+            }
+            if (closest != 0) {
+                g->free_[closest - 1] = 0;
+                g->target[i] = closest;
+                greedy_move_to(g, e, i, closest - 1, 0, mv, op);
+            } else {
+                mv[i] = MV_S;
+                op[i] = 0;
+            }
+        }
+    }
+}

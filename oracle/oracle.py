@@ -70,6 +70,11 @@ def lib():
         L.or_batch_trk.restype = vp
         L.or_batch_trk.argtypes = [vp, i32]
         L.or_batch_step.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32]
+        L.or_greedy_new.restype = vp
+        L.or_greedy_new.argtypes = [i32, i32, i32, i32]
+        L.or_greedy_free.argtypes = [vp]
+        L.or_greedy_init.argtypes = [vp, vp]
+        L.or_greedy_actions.argtypes = [vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -246,3 +251,24 @@ class OracleBatch:
         d = np.zeros(self.E, np.uint8)
         lib().or_batch_step(self.h, _p(a), int(auto_reset), _p(cs), _p(r), _p(sh), _p(d), int(n_threads))
         return r, sh, d.astype(bool)
+
+
+class OracleGreedy:
+    """``GreedyAgents`` (greedyagent.py) restated in C, bug for bug (see mdl_oracle.c)."""
+
+    def __init__(self, env: OracleEnv):
+        self.A = env.A
+        self.h = lib().or_greedy_new(env.A, env.P, env.H, env.W)
+        lib().or_greedy_init(self.h, env.h)       # GreedyAgents(); init_agents(env.reset() state)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_greedy_free(self.h)
+            self.h = None
+
+    def actions(self, env: OracleEnv):
+        """get_actions(state): (move codes S0 L1 R2 U3 D4, op codes 0/1/2) for OracleEnv.step."""
+        mv = np.zeros(self.A, np.uint8)
+        op = np.zeros(self.A, np.uint8)
+        lib().or_greedy_actions(self.h, env.h, _p(mv), _p(op))
+        return mv, op

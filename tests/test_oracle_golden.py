@@ -181,3 +181,26 @@ def test_notebook_kat():
                                       mv, op, k["tracker"], 2, consts)
         assert sh.tobytes().hex() == k[key]
     assert float(np.frombuffer(bytes.fromhex(k["mappo_f32_hex"]), np.float32)[0]) == k["notebook_recorded"]
+
+
+def test_greedy_agent_readme_anchor():
+    """greedyagent.py restated in C reproduces the reference's per-episode greedy results
+    (evaluation.py:9-66 at the README.md:117-121 settings: 34.04 +- 14.83, 3.79 delivered)."""
+    ref = load_json("eval_anchor.json")
+    cfg = ref["config"]
+    g = grid(cfg["map"])
+    rewards, delivered = [], []
+    for ep in range(cfg["episodes"]):
+        env = O.OracleEnv(g, cfg["n_agents"], cfg["n_packages"], cfg["max_time_steps"], seed=cfg["seed"] + ep)
+        env.reset()
+        agent = O.OracleGreedy(env)
+        done = False
+        while not done:
+            mv, op = agent.actions(env)
+            _, _, done = env.step(mv, op)
+        s = env.state()
+        rewards.append(s["total_reward"])
+        delivered.append(int((s["pkgs"][:, 7] == 3).sum()))
+    assert rewards == ref["greedy"]["rewards"]
+    assert delivered == ref["greedy"]["delivered"]
+    assert round(float(np.mean(rewards)), 2) == 34.04 and round(float(np.std(rewards)), 2) == 14.83

@@ -935,3 +935,144 @@ void or_greedy_actions(OGreedy* g, const OEnv* e, uint8_t* mv, uint8_t* op) {
         }
     }
 }
+
+/* ----------------------------------------------------------------------- */
+/* IDQ / qmix featurizers, literal.  Tracker rows are    */
+/* (id, status 1 waiting / 2 in_transit, sr, sc, tr, tc, start, deadline),  */
+/* robots1 are the state's (r+1, c+1, carrying).                            */
+/* ----------------------------------------------------------------------- */
+static double urgency_of(int t, int st, int dl) {
+    double u = 0.0;
+    if (dl > st) {
+        u = (double)(t - st) / (double)(dl - st);
+        u = u > 0.0 ? u : 0.0;
+        u = u < 1.0 ? u : 1.0;
+    } else if (dl == st) {
+        u = t >= st ? 1.0 : 0.0;
+    }
+    return u;
+}
+
+/* IDQ/networks.py:112-217 convert_state (qmix/networks.py:243-348 is the same code) */
+void or_idq_convert_state(const uint8_t* grid, int H, int W, int t, int A, const int32_t* robots1,
+                          const int32_t* trk, int n, int idx, float* out) {
+    memset(out, 0, sizeof(float) * 6 * (size_t)H * W);
+    for (int i = 0; i < H * W; i++) out[i] = (float)grid[i];
+    if (idx < 0 || idx >= A) return;
+    int carried = robots1[3 * idx + 2];
+    if (carried == 0) {
+        for (int k = 0; k < n; k++) {
+            const int32_t* p = trk + 8 * k;
+            if (p[1] != 1) continue;                       /* status == 'waiting' */
+            int sr = p[2], sc = p[3], st = p[6], dl = p[7];
+            if (t >= st) {
+                float u = (float)urgency_of(t, st, dl);
+                if (sr >= 0 && sr < H && sc >= 0 && sc < W) {
+                    float* c1 = &out[1 * H * W + sr * W + sc];
+                    if (u > *c1) *c1 = u;                      /* max(tensor, urgency) */
+                    out[2 * H * W + sr * W + sc] = 1.0f;
+                }
+            }
+        }
+    }
+    for (int i = 0; i < A; i++) {
+        if (i == idx) continue;
+        int r = robots1[3 * i] - 1, c = robots1[3 * i + 1] - 1;
+        if (r >= 0 && r < H && c >= 0 && c < W) out[3 * H * W + r * W + c] = 1.0f;
+    }
+    {
+        int r = robots1[3 * idx] - 1, c = robots1[3 * idx + 1] - 1;
+        if (r >= 0 && r < H && c >= 0 && c < W) out[4 * H * W + r * W + c] = 1.0f;
+    }
+    if (carried != 0) {
+        for (int k = 0; k < n; k++) {
+            const int32_t* p = trk + 8 * k;
+            if (p[0] != carried) continue;                 /* carried id in persistent_packages */
+            int tr = p[4], tc = p[5];
+            if (tr >= 0 && tr < H && tc >= 0 && tc < W) out[5 * H * W + tr * W + tc] = 1.0f;
+            break;
+        }
+    }
+}
+
+/* qmix/networks.py:350-468 convert_global_state_to_tensor, shape (7, oh, ow) */
+void or_qmix_global_tensor(const uint8_t* grid, int H, int W, int t, int A, const int32_t* robots1,
+                           const int32_t* trk, int n, int oh, int ow, float* out) {
+    const size_t S = (size_t)oh * ow;
+    memset(out, 0, sizeof(float) * 7 * S);
+    int sr0 = H > oh ? (H - oh) / 2 : 0, sc0 = W > ow ? (W - ow) / 2 : 0;
+    int rows = H < oh ? H : oh, cols = W < ow ? W : ow;
+    int tro = (oh - rows) / 2, tco = (ow - cols) / 2;
+    for (int r = 0; r < rows; r++)
+        for (int c = 0; c < cols; c++) out[(size_t)(tro + r) * ow + tco + c] = (float)grid[(sr0 + r) * W + sc0 + c];
+    for (int i = 0; i < A; i++) {
+        int r = robots1[3 * i] - 1, c = robots1[3 * i + 1] - 1, cy = robots1[3 * i + 2];
+        if (r >= 0 && r < oh && c >= 0 && c < ow) {
+            out[1 * S + (size_t)r * ow + c] = 1.0f;
+            if (cy != 0) out[2 * S + (size_t)r * ow + c] = 1.0f;
+        }
+    }
+    for (int k = 0; k < n; k++) {
+        const int32_t* p = trk + 8 * k;
+        int sr = p[2], sc = p[3], tr = p[4], tc = p[5], st = p[6], dl = p[7];
+        if (!(t >= st)) continue;
+        if (p[1] == 1) {
+            if (sr >= 0 && sr < oh && sc >= 0 && sc < ow) out[3 * S + (size_t)sr * ow + sc] = 1.0f;
+            if (sr >= 0 && sr < oh && sc >= 0 && sc < ow) {
+                double u = 0.0;
+                if (dl > st) {
+                    u = (double)(t - st) / (double)(dl - st);
+                    u = u > 0.0 ? u : 0.0;
+                    u = u < 1.0 ? u : 1.0;
+                } else if (dl == st) {
+                    u = 1.0;
+                }
+                float* c6 = &out[6 * S + (size_t)sr * ow + sc];
+                if ((float)u > *c6) *c6 = (float)u;
+            }
+            if (tr >= 0 && tr < oh && tc >= 0 && tc < ow) out[4 * S + (size_t)tr * ow + tc] = 1.0f;
+        } else if (p[1] == 2) {
+            if (tr >= 0 && tr < oh && tc >= 0 && tc < ow) out[5 * S + (size_t)tr * ow + tc] = 1.0f;
+        }
+    }
+}
+
+/* IDQ/networks.py:228-349 reward_shaping.  ops: the actions' package ops as ints 0..3;
+ * ops_are_ints = 0 reproduces IDQ/trainer.py's call with string ops ('1' != 1: no op branch). */
+void or_idq_reward_shaping(int prev_t, const int32_t* prev1, int cur_t, const int32_t* cur1, const uint8_t* ops,
+                           int ops_are_ints, const int32_t* trk, int n, int A, double* out) {
+    for (int i = 0; i < A; i++) {
+        double r = 0.0;
+        int pr = prev1[3 * i] - 1, pc = prev1[3 * i + 1] - 1, pcy = prev1[3 * i + 2];
+        int cr = cur1[3 * i] - 1, cc = cur1[3 * i + 1] - 1, ccy = cur1[3 * i + 2];
+        if (pr == cr && pc == cc) r += -0.1;                             /* SHAPING_STAY_PENALTY */
+        int op = ops_are_ints ? ops[i] : -1;
+        if (op == 1) {
+            if (pcy == 0 && ccy != 0) r += 2;                            /* successful pickup */
+            else if (pcy != 0) r += -0.1;
+            else if (pcy == 0 && ccy == 0) {
+                int avail = 0;
+                for (int k = 0; k < n; k++) {
+                    const int32_t* p = trk + 8 * k;
+                    if (p[1] == 1 && p[2] == pr && p[3] == pc && p[6] <= prev_t) { avail = 1; break; }
+                }
+                if (!avail) r += -0.1;
+            }
+        } else if (op == 2) {
+            if (pcy != 0 && ccy == 0) {
+                for (int k = 0; k < n; k++) {
+                    const int32_t* p = trk + 8 * k;
+                    if (p[0] != pcy) continue;
+                    if (cr == p[4] && cc == p[5]) {
+                        r += 10;                                          /* delivery bonus */
+                        if (cur_t > p[7]) r += -5;                        /* late */
+                    }
+                    break;
+                }
+            } else if (pcy == 0) {
+                r += 0;                                                   /* SHAPING_WASTED_DROP_PENALTY */
+            }
+        }
+        out[i] = r;
+    }
+}

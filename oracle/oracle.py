@@ -70,6 +70,9 @@ def lib():
         L.or_batch_trk.restype = vp
         L.or_batch_trk.argtypes = [vp, i32]
         L.or_batch_step.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32]
+        L.or_idq_convert_state.argtypes = [vp, i32, i32, i32, i32, vp, vp, i32, i32, vp]
+        L.or_qmix_global_tensor.argtypes = [vp, i32, i32, i32, i32, vp, vp, i32, i32, i32, vp]
+        L.or_idq_reward_shaping.argtypes = [i32, vp, i32, vp, vp, i32, vp, i32, i32, vp]
         L.or_greedy_new.restype = vp
         L.or_greedy_new.argtypes = [i32, i32, i32, i32]
         L.or_greedy_free.argtypes = [vp]
@@ -272,3 +275,38 @@ class OracleGreedy:
         op = np.zeros(self.A, np.uint8)
         lib().or_greedy_actions(self.h, env.h, _p(mv), _p(op))
         return mv, op
+
+
+def idq_convert_state(grid, t, robots1, trk_rows, idx):
+    """IDQ/networks.py:112-217 (== qmix/networks.py:243-348) convert_state -> f32 [6, H, W]."""
+    g = _c(grid, np.uint8)
+    H, W = g.shape
+    rb = _c(np.asarray(robots1).reshape(-1, 3), np.int32)
+    tr, n = _trk(trk_rows)
+    out = np.zeros((6, H, W), np.float32)
+    lib().or_idq_convert_state(_p(g), H, W, int(t), rb.shape[0], _p(rb), _p(tr), n, int(idx), _p(out))
+    return out
+
+
+def qmix_global_tensor(grid, t, robots1, trk_rows, shape):
+    """qmix/networks.py:350-468 convert_global_state_to_tensor -> f32 [7, oh, ow]."""
+    g = _c(grid, np.uint8)
+    H, W = g.shape
+    rb = _c(np.asarray(robots1).reshape(-1, 3), np.int32)
+    tr, n = _trk(trk_rows)
+    _, oh, ow = shape
+    out = np.zeros((7, oh, ow), np.float32)
+    lib().or_qmix_global_tensor(_p(g), H, W, int(t), rb.shape[0], _p(rb), _p(tr), n, int(oh), int(ow), _p(out))
+    return out
+
+
+def idq_reward_shaping(prev_t, prev_robots1, cur_t, cur_robots1, ops, ops_are_ints, trk_rows, A):
+    """IDQ/networks.py:228-349 reward_shaping -> f64 [A] (ops_are_ints=False: the trainer's string ops)."""
+    pr = _c(np.asarray(prev_robots1).reshape(-1, 3), np.int32)
+    cr = _c(np.asarray(cur_robots1).reshape(-1, 3), np.int32)
+    op = _c(ops, np.uint8)
+    tr, n = _trk(trk_rows)
+    out = np.zeros(A, np.float64)
+    lib().or_idq_reward_shaping(int(prev_t), _p(pr), int(cur_t), _p(cr), _p(op), int(bool(ops_are_ints)), _p(tr), n,
+                                int(A), _p(out))
+    return out

@@ -23,6 +23,9 @@ Fixtures written (all small, compressed):
   kat.json          notebook known-answer test (MAPPO/marl-delivery-mappo.ipynb cell 11)
   eval_anchor.json  evaluation.run_eval('random'/'greedy') per-episode results
                     for the README results table (README.md:117-121)
+  alt_features.npz  IDQ/qmix convert_state, qmix convert_global_state_to_tensor
+                    (incl. cropped/padded shapes), IDQ reward_shaping with int
+                    and string ops   IDQ/networks.py:112-349, qmix/networks.py:243-468
 
 Usage:  python tests/golden/gen_golden.py [--quick]
 """
@@ -524,13 +527,69 @@ def gen_eval_anchor(ref, quick):
         json.dump(res, f)
 
 
+def gen_alt_features(ref, quick):
+    """IDQ / qmix featurizers: IDQ/networks.py:112-217 convert_state,
+    qmix/networks.py:243-348 convert_state, qmix/networks.py:350-468
+    convert_global_state_to_tensor, IDQ/networks.py:228-349 reward_shaping."""
+    idq = _load("ref_idq_networks", os.path.join(REF, "IDQ", "networks.py"))
+    qnet = _load("ref_qmix_networks", os.path.join(REF, "qmix", "networks.py"))
+    rs = np.random.RandomState(2024)
+    grids = {m: ref.env.Environment(map_file(m), 10, 1, 1, seed=0).grid for m in ["map1.txt", "map2.txt", "map.txt"]}
+    cases, arrays = [], {}
+    n = 30 if quick else 120
+    for i in range(n):
+        m = ["map1.txt", "map2.txt", "map.txt"][i % 3]
+        grid = grids[m]
+        H, W = len(grid), len(grid[0])
+        A = int(rs.choice([1, 2, 5, 8]))
+        t = int(rs.randint(0, 120))
+        state, trk = random_dict_case(rs, grid, A, int(rs.randint(0, 25)), t, id_max=30)
+        obs_i = np.stack([idq.convert_state(state, trk, a) for a in range(A)])
+        obs_q = np.stack([qnet.convert_state(state, trk, a) for a in range(A)])
+        shapes = [(7, H, W), (7, max(1, H - int(rs.randint(0, 4))), W + int(rs.randint(0, 5))),
+                  (7, H + int(rs.randint(1, 6)), max(1, W - int(rs.randint(1, 4))))]
+        gst = [qnet.convert_global_state_to_tensor(state, trk, sh) for sh in shapes]
+        # IDQ reward shaping: next state = robots moved / carry changed at random
+        free = [(a, b) for a in range(H) for b in range(W) if grid[a][b] == 0]
+        cur_robots = []
+        for (r, c, cy) in state["robots"]:
+            if rs.random_sample() < 0.5:
+                fr = free[rs.randint(len(free))]
+                r, c = fr[0] + 1, fr[1] + 1
+            if rs.random_sample() < 0.4:
+                cy = 0 if cy else int(rs.randint(1, 31))
+            cur_robots.append((r, c, cy))
+        cur = {"time_step": t + 1, "map": grid, "robots": cur_robots, "packages": []}
+        ops = [int(rs.randint(0, 4)) for _ in range(A)]
+        acts_int = [("S", o) for o in ops]                       # docstring form: int ops
+        acts_str = [("S", str(o)) for o in ops]                  # IDQ/trainer.py:280-300 passes strings
+        rw_int = idq.reward_shaping(state, cur, acts_int, trk, A)
+        rw_str = idq.reward_shaping(state, cur, acts_str, trk, A)
+        arrays[f"robots_{i}"] = np.array(state["robots"], np.int32).reshape(-1, 3)
+        arrays[f"cur_robots_{i}"] = np.array(cur_robots, np.int32).reshape(-1, 3)
+        arrays[f"trk_{i}"] = np.array([[v["id"], 1 if v["status"] == "waiting" else 2, v["start_pos"][0],
+                                        v["start_pos"][1], v["target_pos"][0], v["target_pos"][1], v["start_time"],
+                                        v["deadline"]] for v in trk.values()], np.int32).reshape(-1, 8)
+        arrays[f"ops_{i}"] = np.array(ops, np.uint8)
+        arrays[f"idq_obs_{i}"] = obs_i.astype(np.float32)
+        arrays[f"qmix_obs_{i}"] = obs_q.astype(np.float32)
+        for k, g in enumerate(gst):
+            arrays[f"qmix_state_{i}_{k}"] = g.astype(np.float32)
+        arrays[f"rw_int_{i}"] = np.array(rw_int, np.float64)
+        arrays[f"rw_str_{i}"] = np.array(rw_str, np.float64)
+        cases.append(dict(map=m, A=A, t=t, shapes=[list(sh) for sh in shapes]))
+    arrays["meta"] = np.frombuffer(json.dumps(cases).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "alt_features.npz"), **arrays)
+    print("alt feature cases", len(cases))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     ref = load_reference()
-    todo = args.only.split(",") if args.only else ["reset", "steps", "mappo", "qmix", "helpers", "kat", "eval"]
+    todo = args.only.split(",") if args.only else ["reset", "steps", "mappo", "qmix", "helpers", "kat", "eval", "alt"]
     if "reset" in todo:
         gen_reset(ref, args.quick)
     if "steps" in todo:
@@ -550,6 +609,8 @@ def main():
         gen_kat(ref)
     if "eval" in todo:
         gen_eval_anchor(ref, args.quick)
+    if "alt" in todo:
+        gen_alt_features(ref, args.quick)
 
 
 if __name__ == "__main__":

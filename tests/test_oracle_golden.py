@@ -204,3 +204,22 @@ def test_greedy_agent_readme_anchor():
     assert rewards == ref["greedy"]["rewards"]
     assert delivered == ref["greedy"]["delivered"]
     assert round(float(np.mean(rewards)), 2) == 34.04 and round(float(np.std(rewards)), 2) == 14.83
+
+
+def test_alt_featurizers_golden():
+    """IDQ/qmix convert_state, qmix convert_global_state_to_tensor (incl. cropped/padded
+    shapes) and IDQ reward_shaping (int and string ops) vs the reference's outputs."""
+    d = npz("alt_features.npz")
+    for i, c in enumerate(meta(d)):
+        g = grid(c["map"])
+        rob, trk, t, A = d[f"robots_{i}"], d[f"trk_{i}"], c["t"], c["A"]
+        for a in range(A):
+            np.testing.assert_array_equal(O.idq_convert_state(g, t, rob, trk, a), d[f"idq_obs_{i}"][a], f"idq {i}/{a}")
+        for k, sh in enumerate(c["shapes"]):
+            np.testing.assert_array_equal(O.qmix_global_tensor(g, t, rob, trk, sh), d[f"qmix_state_{i}_{k}"],
+                                          f"qmix state {i}/{k}")
+        cur = d[f"cur_robots_{i}"]
+        np.testing.assert_array_equal(O.idq_reward_shaping(t, rob, t + 1, cur, d[f"ops_{i}"], True, trk, A),
+                                      d[f"rw_int_{i}"], f"rw int {i}")
+        np.testing.assert_array_equal(O.idq_reward_shaping(t, rob, t + 1, cur, d[f"ops_{i}"], False, trk, A),
+                                      d[f"rw_str_{i}"], f"rw str {i}")

@@ -98,6 +98,26 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
 int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
                    int32_t k_steps, int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
 
+/* ---- IDQ / qmix featurizers and IDQ reward shaping ----
+ * mdl_build_obs_alt, for envs [env_begin, env_begin+n) sharing one map shape (H, W):
+ *   idq_obs    f32 [n][A][6][H][W]       convert_state                IDQ/networks.py:112-217
+ *                                        (qmix/networks.py:243-348 is the same function)
+ *   qmix_state f32 [n][7][out_h][out_w]  convert_global_state_to_tensor qmix/networks.py:350-468
+ *                                        with state_tensor_shape (7, out_h, out_w); the trainers pass (7, H, W)
+ * Either pointer may be NULL.  The IDQ / qmix trainers clear their tracker per episode: build the
+ * engine with MDL_TRACKER_FRESH for them.
+ * mdl_views_alt_features: the same on packed dict views (as mdl_views_features).
+ * mdl_views_idq_reward: reward_shaping (IDQ/networks.py:228-349) per agent, fp64, out[op_offsets[w]+a];
+ * ops_are_ints = 0 reproduces IDQ/trainer.py, which passes string ops (so no op branch fires). */
+int mdl_build_obs_alt(MdlEngine* eng, int32_t env_begin, int32_t n, float* idq_obs, float* qmix_state, int32_t out_h,
+                      int32_t out_w, void* stream);
+int mdl_views_alt_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
+                           int32_t max_slots, const int32_t* agent_idx, float* idq_obs, float* qmix_state,
+                           int32_t out_h, int32_t out_w, void* stream);
+int mdl_views_idq_reward(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets, int32_t max_slots,
+                         const int32_t* cur, const int64_t* cur_offsets, const uint8_t* ops, const int64_t* op_offsets,
+                         int32_t ops_are_ints, int32_t n, double* out, void* stream);
+
 /* ---- greedy baseline: greedyagent.py batched on the device ----
  * mdl_greedy_init = GreedyAgents() + init_agents(state) for the listed envs (call it right
  * after their reset, as evaluation.py:29-35 does); the first call also builds run_bfs's

@@ -579,6 +579,55 @@ int mdl_views_shaped_reward(MdlEngine* eng, const int32_t* prev_views, const int
     return 0;
 }
 
+// ---- IDQ / qmix featurizers and IDQ reward shaping ----
+int mdl_build_obs_alt(MdlEngine* eng, int32_t env_begin, int32_t n, float* idq_obs, float* qmix_state, int32_t out_h,
+                      int32_t out_w, void* stream) {
+    if (!eng) return fail("mdl_build_obs_alt: null engine");
+    if (env_begin < 0 || n < 0 || env_begin + n > eng->p.E) return fail("mdl_build_obs_alt: env range out of bounds");
+    if (qmix_state && (out_h < 1 || out_w < 1 || out_h > 4096 || out_w > 4096))
+        return fail("mdl_build_obs_alt: bad state tensor shape (%d, %d)", out_h, out_w);
+    if (n == 0) return 0;
+    const size_t lds = mdl::alt_obs_lds(eng->p.P, eng->maxHW);
+    const int wpb = waves_per_block(lds);
+    if (wpb < 1) return fail("mdl_build_obs_alt: needs %zu bytes of LDS per env", lds);
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_alt_obs(eng->p, env_begin, n, idq_obs, qmix_state, out_h, out_w, wpb, lds,
+                               (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_views_alt_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
+                           int32_t max_slots, const int32_t* agent_idx, float* idq_obs, float* qmix_state,
+                           int32_t out_h, int32_t out_w, void* stream) {
+    if (!eng || !views || !offsets) return fail("mdl_views_alt_features: null argument");
+    if (n_views < 0 || max_slots < 0 || max_slots > 4096) return fail("mdl_views_alt_features: bad sizes");
+    if (qmix_state && (out_h < 1 || out_w < 1 || out_h > 4096 || out_w > 4096))
+        return fail("mdl_views_alt_features: bad state tensor shape (%d, %d)", out_h, out_w);
+    if (n_views == 0) return 0;
+    const size_t lds = mdl::views_alt_lds(max_slots, eng->maxHW);
+    const int wpb = waves_per_block(lds);
+    if (wpb < 1) return fail("mdl_views_alt_features: needs %zu bytes of LDS per view", lds);
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_views_alt(eng->p, views, offsets, n_views, agent_idx, idq_obs, qmix_state, out_h, out_w, wpb,
+                                 lds, max_slots, (hipStream_t)stream));
+    return 0;
+}
+
+int mdl_views_idq_reward(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets, int32_t max_slots,
+                         const int32_t* cur, const int64_t* cur_offsets, const uint8_t* ops, const int64_t* op_offsets,
+                         int32_t ops_are_ints, int32_t n, double* out, void* stream) {
+    if (!eng || !prev_views || !prev_offsets || !cur || !cur_offsets || !ops || !op_offsets || !out)
+        return fail("mdl_views_idq_reward: null argument");
+    if (n < 0 || max_slots < 0 || max_slots > 4096) return fail("mdl_views_idq_reward: bad sizes");
+    if (n == 0) return 0;
+    const size_t lds = mdl::views_shaped_lds(max_slots);
+    const int wpb = waves_per_block(lds);
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_views_idq_reward(prev_views, prev_offsets, cur, cur_offsets, ops, op_offsets, ops_are_ints, n,
+                                        out, wpb, lds, max_slots, (hipStream_t)stream));
+    return 0;
+}
+
 int mdl_rank_table(int32_t H, int32_t W, uint16_t* out) {
     if (!out || H < 1 || W < 1 || H > 255 || W > 255) return fail("mdl_rank_table: bad arguments");
     std::vector<uint16_t> rk;

@@ -19,6 +19,7 @@
 // readlane / ballot only; LDS is touched only when an env resets.
 #include "mdl_kernels.hpp"
 #include "mdl_features.hpp"
+#include "mdl_altfeat.hpp"
 
 // Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
 // reward, 2 the tracker update, 4 movement, 8 package actions, 16 the move-validity
@@ -663,6 +664,16 @@ __host__ __device__ inline size_t obs_pre_bytes(int P) {
     return align16(8 * (size_t)P) * 2 + align16(4 * (size_t)P) + align16((size_t)P);
 }
 
+__device__ inline ObsLdsPre obs_pre_carve(unsigned char* base, int P) {
+    ObsLdsPre S;
+    size_t o = 0;
+    S.pk = (uint64_t*)(base + o); o += align16(8 * (size_t)P);
+    S.td = (uint64_t*)(base + o); o += align16(8 * (size_t)P);
+    S.tq = (uint32_t*)(base + o); o += align16(4 * (size_t)P);
+    S.ps = base + o;
+    return S;
+}
+
 template <bool STALE>
 __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, float* __restrict__ amap,
                                              float* __restrict__ avec, float* __restrict__ cmap,
@@ -675,14 +686,7 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
     const int e = env_begin + w;
     const int A = p.A, P = p.P;
     unsigned char* base = smem + (size_t)wave * lds_stride;
-    ObsLdsPre S;
-    {
-        size_t o = 0;
-        S.pk = (uint64_t*)(base + o); o += align16(8 * (size_t)P);
-        S.td = (uint64_t*)(base + o); o += align16(8 * (size_t)P);
-        S.tq = (uint32_t*)(base + o); o += align16(4 * (size_t)P);
-        S.ps = base + o;
-    }
+    ObsLdsPre S = obs_pre_carve(base, P);
     const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
     FeatCtx c;
     c.A = A; c.NS = P; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.NW = (c.HW + 31) / 32;
@@ -852,6 +856,110 @@ __global__ __launch_bounds__(256) void k_views_shaped(DevParams p, const int32_t
     if (lane == 0) out[w] = res;
 }
 
+// ------------------------------------------------- IDQ / qmix featurizers
+// convert_state for every agent and convert_global_state_to_tensor (7, oh, ow)
+// from the engine state + tracker.
+template <bool STALE>
+__global__ __launch_bounds__(256) void k_alt_obs(DevParams p, int env_begin, int n, float* __restrict__ idq,
+                                                 float* __restrict__ qst, int oh, int ow, int wpb, int lds_stride) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int wave = wave_id();
+    const int lane = lane_id();
+    const int w = blockIdx.x * wpb + wave;
+    if (wave >= wpb || w >= n) return;
+    const int e = env_begin + w;
+    const int A = p.A, P = p.P;
+    unsigned char* base = smem + (size_t)wave * lds_stride;
+    ObsLdsPre S = obs_pre_carve(base, P);
+    const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
+    const int H = md.H, W = md.W;
+    AltLds L = alt_carve(base + obs_pre_bytes(P), H * W);
+    const bool act = lane < A;
+    const uint32_t rv = act ? p.rob[(size_t)e * A + lane] : 0u;
+    const int cell = rob_cell(rv), carry = rob_carry(rv);
+    const int t = p.es[e].t;
+    for (int j = lane; j < P; j += WAVE) {
+        const size_t g = (size_t)e * P + j;
+        const uint64_t d = p.pkg[g];
+        const uint32_t f = p.pstate[g];
+        S.pk[j] = d;
+        S.ps[j] = (uint8_t)(f & PS_FLAGS);
+        if (STALE) {
+            const bool sv = (f & PS_SURVIVOR) != 0;
+            S.td[j] = sv ? p.trk[g] : d;
+            S.tq[j] = sv ? f >> PS_RANK_SHIFT : ORD_EPISODE + (uint32_t)j;
+        }
+    }
+    wave_sync();
+    const uint8_t* grid = p.grids + md.grid_off;
+    auto run = [&](const auto& trk) {
+        alt_prepare(trk, H * W, W, A, t, cell, carry, L);
+        if (idq) alt_emit_idq(trk, grid, H, W, L, cell, carry, 0, A, true, idq + (size_t)w * A * 6 * H * W);
+        if (qst) alt_emit_qmix(grid, H, W, L, oh, ow, qst + (size_t)w * 7 * oh * ow);
+    };
+    if (STALE) {
+        TrkStale trk{S.ps, S.td, S.tq, P};
+        run(trk);
+    } else {
+        TrkFresh trk{S.pk, S.ps, P};
+        run(trk);
+    }
+}
+
+// The same builders on packed dict views (one agent index per view).
+__global__ __launch_bounds__(256) void k_views_alt(DevParams p, const int32_t* __restrict__ views,
+                                                   const int64_t* __restrict__ offs, int n,
+                                                   const int32_t* __restrict__ agent_idx, float* __restrict__ idq,
+                                                   float* __restrict__ qst, int oh, int ow, int wpb, int lds_stride,
+                                                   int NSmax) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int wave = wave_id();
+    const int w = blockIdx.x * wpb + wave;
+    if (wave >= wpb || w >= n) return;
+    unsigned char* base = smem + (size_t)wave * lds_stride;
+    ViewLdsPre V = view_carve(base, NSmax);
+    int t, A, map, cell, carry;
+    const TrkView trk = load_view(views + offs[w], V, t, A, map, cell, carry);
+    wave_sync();
+    const MapDesc md = p.maps[map];
+    const int H = md.H, W = md.W;
+    AltLds L = alt_carve(base + view_pre_bytes(NSmax), H * W);
+    alt_prepare(trk, H * W, W, A, t, cell, carry, L);
+    const uint8_t* grid = p.grids + md.grid_off;
+    const int a = agent_idx ? agent_idx[w] : 0;
+    const bool valid = a >= 0 && a < A;
+    if (idq) alt_emit_idq(trk, grid, H, W, L, cell, carry, valid ? a : 0, 1, valid, idq + (size_t)w * 6 * H * W);
+    if (qst) alt_emit_qmix(grid, H, W, L, oh, ow, qst + (size_t)w * 7 * oh * ow);
+}
+
+// IDQ reward_shaping on packed views: out[op_offs[w] + a] (fp64), ops_are_ints = 0
+// reproduces IDQ/trainer.py's string ops.
+__global__ __launch_bounds__(256) void k_views_idq_reward(const int32_t* __restrict__ prev,
+                                                          const int64_t* __restrict__ prev_offs,
+                                                          const int32_t* __restrict__ cur,
+                                                          const int64_t* __restrict__ cur_offs,
+                                                          const uint8_t* __restrict__ ops,
+                                                          const int64_t* __restrict__ op_offs, int ops_are_ints, int n,
+                                                          double* __restrict__ out, int wpb, int lds_stride,
+                                                          int NSmax) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int wave = wave_id();
+    const int lane = lane_id();
+    const int w = blockIdx.x * wpb + wave;
+    if (wave >= wpb || w >= n) return;
+    ViewLdsPre V = view_carve(smem + (size_t)wave * lds_stride, NSmax);
+    int t_prev, A, map, pcell, pcarry;
+    const TrkView trk = load_view(prev + prev_offs[w], V, t_prev, A, map, pcell, pcarry);
+    wave_sync();
+    const int32_t* cr = cur + cur_offs[w];
+    if (lane < A) {
+        const int ccell = cr[2 + 3 * lane] | (cr[3 + 3 * lane] << 8);
+        const int ccarry = cr[4 + 3 * lane];
+        const int op = ops_are_ints ? (int)ops[op_offs[w] + lane] : -1;
+        out[op_offs[w] + lane] = idq_reward(trk, pcell, pcarry, ccell, ccarry, op, t_prev, cr[0]);
+    }
+}
+
 // ------------------------------------------------------------ state export
 // int32 views of the SoA state for the dict-compat layer and the tests.
 __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict__ robots, int32_t* __restrict__ pkgs,
@@ -977,6 +1085,37 @@ hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, cons
                        double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
     if (p.stale) launch_step_s<true, false>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, 1, s);
     else launch_step_s<false, false>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, 1, s);
+    return hipGetLastError();
+}
+
+size_t alt_obs_lds(int P, int HW) { return obs_pre_bytes(P) + alt_lds_bytes(HW); }
+size_t views_alt_lds(int NSmax, int HW) { return view_pre_bytes(NSmax) + alt_lds_bytes(HW); }
+
+hipError_t launch_alt_obs(const DevParams& p, int env_begin, int n, float* idq, float* qst, int oh, int ow, int wpb,
+                          size_t lds, hipStream_t s) {
+    if (p.stale)
+        hipLaunchKernelGGL(k_alt_obs<true>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin, n, idq,
+                           qst, oh, ow, wpb, (int)lds);
+    else
+        hipLaunchKernelGGL(k_alt_obs<false>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin, n, idq,
+                           qst, oh, ow, wpb, (int)lds);
+    return hipGetLastError();
+}
+
+hipError_t launch_views_alt(const DevParams& p, const int32_t* views, const int64_t* offs, int n,
+                            const int32_t* agent_idx, float* idq, float* qst, int oh, int ow, int wpb, size_t lds,
+                            int NSmax, hipStream_t s) {
+    hipLaunchKernelGGL(k_views_alt, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, views, offs, n, agent_idx,
+                       idq, qst, oh, ow, wpb, (int)lds, NSmax);
+    return hipGetLastError();
+}
+
+hipError_t launch_views_idq_reward(const int32_t* prev, const int64_t* prev_offs, const int32_t* cur,
+                                   const int64_t* cur_offs, const uint8_t* ops, const int64_t* op_offs,
+                                   int ops_are_ints, int n, double* out, int wpb, size_t lds, int NSmax,
+                                   hipStream_t s) {
+    hipLaunchKernelGGL(k_views_idq_reward, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, prev, prev_offs, cur,
+                       cur_offs, ops, op_offs, ops_are_ints, n, out, wpb, (int)lds, NSmax);
     return hipGetLastError();
 }
 

@@ -43,6 +43,18 @@ hipError_t launch_greedy_init(const DevParams& p, const GreedyLayout& g, unsigne
 hipError_t launch_greedy_act(const DevParams& p, const GreedyLayout& g, unsigned char* gs, const uint16_t* tables,
                              const int* ids, int n, uint8_t* actions, hipStream_t s);
 
+hipError_t launch_alt_obs(const DevParams& p, int env_begin, int n, float* idq, float* qst, int oh, int ow, int wpb,
+                          size_t lds, hipStream_t s);
+hipError_t launch_views_alt(const DevParams& p, const int32_t* views, const int64_t* offs, int n,
+                            const int32_t* agent_idx, float* idq, float* qst, int oh, int ow, int wpb, size_t lds,
+                            int NSmax, hipStream_t s);
+hipError_t launch_views_idq_reward(const int32_t* prev, const int64_t* prev_offs, const int32_t* cur,
+                                   const int64_t* cur_offs, const uint8_t* ops, const int64_t* op_offs,
+                                   int ops_are_ints, int n, double* out, int wpb, size_t lds, int NSmax,
+                                   hipStream_t s);
+size_t alt_obs_lds(int P, int HW);
+size_t views_alt_lds(int NSmax, int HW);
+
 size_t step_lds(int P);
 size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs);
 size_t views_lds(int NSmax, int HW, int MO, int MPc, int MR, int MPsc);

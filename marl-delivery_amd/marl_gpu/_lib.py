@@ -56,6 +56,9 @@ SIGNATURES = {
     "mdl_step": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mdl_step_fused": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mdl_build_obs": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "mdl_build_obs_alt": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp]),
+    "mdl_views_alt_features": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp]),
+    "mdl_views_idq_reward": (C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp]),
     "mdl_greedy_init": (C.c_int, [_vp, _vp, _i32, _vp]),
     "mdl_greedy_actions": (C.c_int, [_vp, _vp, _i32, _vp, _vp]),
     "mdl_state_bytes": (C.c_int, [_vp, C.POINTER(C.c_int64)]),

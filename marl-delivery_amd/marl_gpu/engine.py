@@ -221,6 +221,28 @@ class BatchedEnv:
                                   ptr(p["critic_map"]), ptr(p["critic_vec"]), self._stream()), "mdl_build_obs")
         return out
 
+    # ---- IDQ / qmix featurizers ----
+    def build_obs_alt(self, env_begin: int = 0, n: int | None = None, out: dict | None = None,
+                      state_shape=None, which=("idq_obs", "qmix_state")):
+        """convert_state for every agent (IDQ/networks.py:112-217, == qmix/networks.py:243-348) and
+        convert_global_state_to_tensor (qmix/networks.py:350-468) for envs [env_begin, env_begin+n).
+        state_shape (7, h, w) defaults to the map's (7, H, W) as the qmix trainer uses; build the
+        engine with tracker="fresh" for the IDQ / qmix trainers' per-episode trackers."""
+        n = self.E - env_begin if n is None else n
+        g = self.grids[int(self.env_map[env_begin])] if n else self.grids[0]
+        H, W = g.shape
+        oh, ow = (H, W) if state_shape is None else (int(state_shape[1]), int(state_shape[2]))
+        if out is None:
+            f = dict(dtype=torch.float32, device=self.device)
+            out = {}
+            if "idq_obs" in which:
+                out["idq_obs"] = torch.empty((n, self.A, 6, H, W), **f)
+            if "qmix_state" in which:
+                out["qmix_state"] = torch.empty((n, 7, oh, ow), **f)
+        check(lib().mdl_build_obs_alt(self._h, env_begin, n, ptr(out.get("idq_obs")), ptr(out.get("qmix_state")),
+                                      oh, ow, self._stream()), "mdl_build_obs_alt")
+        return out
+
     # ---- greedy baseline (SURVEY.md §8(f)3): greedyagent.py batched on the device ----
     def greedy_init(self, env_ids=None):
         """``GreedyAgents()`` + ``init_agents(state)`` for the listed envs (right after their reset)."""

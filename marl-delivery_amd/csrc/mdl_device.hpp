@@ -65,6 +65,7 @@ struct DevParams {
     int stale;
     int obsT, MO, MP, MR, MPs;
     int n_maps;
+    int key32_dsh;  // > 0: the obs sort keys (dlc, rank, order) fit 32 bits, dlc at this shift
     MapDesc maps[MAX_MAPS];
     const uint8_t* grids;
     const uint8_t* movevalid;  // per map cell: bit m set if move code m (L,R,U,D = 1..4) stays on a free cell

@@ -169,6 +169,8 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
 
     // ---- maps ----
     std::vector<uint8_t> allgrid, allvalid;
+    int rank_max = 0;
+    long dl_max = 0;
     std::vector<uint32_t> allbits;
     std::vector<uint16_t> allfree, allrank;
     mdl::DevParams& p = eng->p;
@@ -229,6 +231,8 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         }
         std::vector<uint16_t> rk;
         build_rank(H, W, rk);
+        for (uint16_t v : rk) rank_max = std::max<int>(rank_max, v);
+        dl_max = std::max<long>(dl_max, (long)c.max_time_steps - 1 + 10 + 3L * H);
         allrank.insert(allrank.end(), rk.begin(), rk.end());
         eng->mapH.push_back(H);
         eng->mapW.push_back(W);
@@ -263,6 +267,11 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     p.MR = c.max_robots_state;
     p.MPs = c.max_packages_state;
     p.n_maps = n_maps;
+    {   // 32-bit obs sort keys: order (11 bits) | rank << 11 | max(0, dl - t) << (11 + rank bits)
+        auto bits = [](long v) { int b = 0; while (v > 0) { b++; v >>= 1; } return b; };
+        const int rb = bits(rank_max), db = bits(dl_max);
+        p.key32_dsh = (11 + rb + db <= 32) ? 11 + rb : 0;
+    }
 
     const size_t E = c.n_envs, A = c.n_robots, P = c.n_packages;
     uint8_t *d_grid = nullptr, *d_valid = nullptr;

@@ -271,6 +271,69 @@ __device__ inline void feat_sort_agent(const Trk& trk, const FeatCtx& c, FeatLds
     wave_sync();
 }
 
+// All agents' waiting-package selections at once (engine path: NS <= 64 slots,
+// A <= AMAX, and (dlc, rank, order) packed into 32 bits -- the host checks the
+// bit budget, DevParams::key32_dsh): the per-slot fields are computed once, the
+// A rank-table gathers issue together, and the A selection chains (one wave
+// minimum per wanted slot) interleave.  Same order as feat_sort_agent's
+// (dlc, rank, order) 64-bit keys.
+template <class Trk, int AMAX>
+__device__ inline void feat_sort_pkgs_fast(const Trk& trk, const FeatCtx& c, FeatLds& L, int dsh) {
+    const int lane = lane_id();
+    const int A = c.A, t = c.t;
+    bool wv = false;
+    int dlc = 0, sr = 0, scc = 0;
+    uint32_t ord = 0;
+    if (lane < c.NS && trk.present(lane) && !trk.in_transit(lane)) {
+        const uint64_t d = trk.data(lane);
+        if (pk_st(d) <= t) {
+            wv = true;
+            dlc = pk_dl(d) - t;
+            if (dlc < 0 || c.T <= 0) dlc = 0;
+            sr = cell_r(pk_start(d));
+            scc = cell_c(pk_start(d));
+            ord = trk.order(lane);
+        }
+    }
+    const int np = popc64(ballot(wv));
+    const int want = np < c.MPc ? np : c.MPc;
+    uint32_t key[AMAX];
+#pragma unroll
+    for (int a = 0; a < AMAX; a++) {
+        const int aa = a < A ? a : 0;
+        const int ra = L.rr[aa], ca = L.rcol[aa];
+        key[a] = (wv && a < A) ? ((uint32_t)dlc << dsh) | ((uint32_t)rank_of(c, sr - ra, scc - ca) << 11) | ord
+                               : 0xffffffffu;
+    }
+    for (int s = 0; s < want; s++) {
+#pragma unroll
+        for (int a = 0; a < AMAX; a++) {
+            if (a < A) {
+                const uint32_t m = wave_min_u32(key[a]);
+                if (key[a] == m) {
+                    L.inv_p[a * c.MPc + s] = (uint16_t)lane;
+                    key[a] = 0xffffffffu;
+                }
+            }
+        }
+    }
+    if (lane < A) L.cnt[lane] = (A - 1) | (np << 8);
+    wave_sync();
+}
+
+// The other-robot half of feat_sort_agent (for use beside feat_sort_pkgs_fast).
+__device__ inline void feat_sort_others(const FeatCtx& c, FeatLds& L, int a, int cell) {
+    const int lane = lane_id();
+    const int A = c.A;
+    const int ra = L.rr[a], ca = L.rcol[a];
+    const bool valid = lane < A && lane != a;
+    int key = 0x7fffffff;
+    if (valid) key = (rank_of(c, cell_r(cell) - ra, cell_c(cell) - ca) << 8) | lane;
+    int pos = 0;
+    for (int o = 0; o < A; o++) pos += rdl(key, o) < key;
+    if (valid && pos < c.MO) L.inv_o[a * 64 + pos] = (uint8_t)lane;
+}
+
 __device__ __forceinline__ float dlc_over_T(int dl, int t, int T) {
     if (T <= 0) return 0.0f;
     int d = dl - t;

@@ -723,7 +723,12 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
         if (amap) emit_actor_maps(c, L, 0, A, true, amap + le * (size_t)A * 6 * c.HW);
         if (cmap) emit_critic_map(c, L, cmap + le * 4 * (size_t)c.HW);
         if (avec) {
-            for (int a = 0; a < A; a++) feat_sort_agent(trk, c, L, a, cell);
+            if (p.key32_dsh > 0 && P <= WAVE && A <= 8) {
+                for (int a = 0; a < A; a++) feat_sort_others(c, L, a, cell);
+                feat_sort_pkgs_fast<decltype(trk), 8>(trk, c, L, p.key32_dsh);
+            } else {
+                for (int a = 0; a < A; a++) feat_sort_agent(trk, c, L, a, cell);
+            }
             const int Dv = 6 + 5 * c.MO + 5 * c.MP + 1;
             emit_actor_vecs(trk, c, L, 0, A, true, avec + le * (size_t)A * Dv);
         }

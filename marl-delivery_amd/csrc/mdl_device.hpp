@@ -447,6 +447,23 @@ __device__ inline float shaped_agent(const Trk& trk, const float* C, bool active
     return active ? s : 0.0f;
 }
 
+// np_sum_lanes for n <= 8 (the sequential n < 8 branch, and the 8-partial form at n == 8),
+// with the readlanes issued up front.
+__device__ inline float np_sum_lanes8(float v, int n) {
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = rdlf(v, i);
+    float res;
+    if (n == 8) {
+        res = ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
+    } else {
+        res = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 7; i++) res = i < n ? res + x[i] : res;
+    }
+    return 0.0f + res;
+}
+
 // numpy float32 add.reduce over lanes 0..n-1 (n <= 64): 0 + pairwise_sum
 // (8 running partials for n >= 8, sequential tail).  Wave-uniform result.
 __device__ inline float np_sum_lanes(float v, int n) {

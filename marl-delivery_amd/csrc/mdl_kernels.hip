@@ -103,7 +103,7 @@ __device__ inline int do_reset(const DevParams& p, int e, const MapDesc& md, Res
 // insert ids spawned at t that are absent (in id order), then carried ->
 // in_transit, in_transit & not carried -> delete.  An inserted entry's order
 // key is implicit (ORD_EPISODE + slot) until the next reset.
-template <int NCH>
+template <int NCH, bool SMALL = false>
 __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[NCH], bool (&dirty)[NCH],
                                            const uint64_t (&pk)[NCH], int P, int A, int carry, int t) {
     const int lane = lane_id();
@@ -120,7 +120,12 @@ __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[N
     for (int c = 0; c < NCH; c++) {
         const int id = c * WAVE + lane + 1;
         bool carried = false;
-        for (int i = 0; i < A; i++) carried |= rdl(carry, i) == id;
+        if constexpr (SMALL) {  // A <= 8: lanes >= A carry 0 and ids start at 1, so no bound is needed
+#pragma unroll
+            for (int i = 0; i < 8; i++) carried |= rdl(carry, i) == id;
+        } else {
+            for (int i = 0; i < A; i++) carried |= rdl(carry, i) == id;
+        }
         if (ps[c] & PS_PRESENT) {
             if (carried) ps[c] |= PS_TRANSIT;
             else if (ps[c] & PS_TRANSIT) ps[c] &= PS_STATUS;
@@ -273,7 +278,9 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 #else
 #define MDL_STEP_LB (64 * MDL_STEP_WPB)
 #endif
-template <bool STALE, int NCH, bool FUSED>
+// SMALL: A <= 8 robots -- the per-robot scans are unrolled over 8 lanes (independent
+// readlanes, no loop-carried branch), the latency-critical form at the configs' A = 5.
+template <bool STALE, int NCH, bool FUSED, bool SMALL>
 __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t* __restrict__ actions, int fmt,
                                               const int* __restrict__ env_ids, int n, int auto_reset,
                                               double* __restrict__ r_out, float* __restrict__ sh_out,
@@ -378,30 +385,59 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
         // winner = lowest-index mover into the cell: the reference's restart-from-0
         // loop, checked against the oracle's literal restatement.
         const int pcell = cell, pcarry = carry;
-        int prop = cell;
-        if (act && ((vmask >> mv) & 1u)) {  // bits 1..4 only: S / other moves never move
-            const int m = mv <= MV_R ? 256 : 1;  // L -256, R +256, U -1, D +1
-            prop = cell + ((mv & 1) ? -m : m);
-        }
+        // bits 1..4 of vmask only: S / other moves never move; L -256, R +256, U -1, D +1
+        const int dm = mv <= MV_R ? 256 : 1;
+        const int prop = cell + ((act && ((vmask >> mv) & 1u)) ? ((mv & 1) ? -dm : dm) : 0);
         const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
         const uint64_t movers = ballot(mover);
         uint64_t moved = 0;
+        STAMP(12);
         if (movers) {
             // blocked: a lower-index mover proposes the same cell; occ: the robot
             // now standing on the proposed cell (robots stand on distinct cells)
             int blocked = 0, occ = -1;
-            for (uint64_t m = movers; m; m &= m - 1) {
-                const int j = ffs64(m);
-                blocked |= (int)(j < lane) & (int)(rdl(prop, j) == prop);
+            if constexpr (SMALL) {
+                // Every test is one compare of this lane's proposal against a scalar, and the
+                // per-j answers combine as wave masks in scalar registers (no lane-serial chain):
+                //   blocked: lanes above j where mover j proposes the same cell
+                //   occ:     the (unique) robot j standing on the proposed cell, as 3 bits
+                const uint32_t mv32 = (uint32_t)movers;
+                uint64_t bl = 0, has = 0, o0 = 0, o1 = 0, o2 = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint64_t above = ((mv32 >> j) & 1u) ? (~0ull << (j + 1)) : 0ull;
+                    bl |= ballot(rdl(prop, j) == prop) & above;
+                    const uint64_t m = ballot(rdl(cell, j) == prop) & (j < A ? ~0ull : 0ull);
+                    has |= m;
+                    if (j & 1) o0 |= m;
+                    if (j & 2) o1 |= m;
+                    if (j & 4) o2 |= m;
+                }
+                blocked = (int)((bl >> lane) & 1ull);
+                occ = ((has >> lane) & 1ull) ? (int)(((o0 >> lane) & 1ull) | (((o1 >> lane) & 1ull) << 1) |
+                                                     (((o2 >> lane) & 1ull) << 2))
+                                             : -1;
+            } else {
+                for (uint64_t m = movers; m; m &= m - 1) {
+                    const int j = ffs64(m);
+                    blocked |= (int)(j < lane) & (int)(rdl(prop, j) == prop);
+                }
+                for (int j = 0; j < A; j++) occ = rdl(cell, j) == prop ? j : occ;
             }
-            for (int j = 0; j < A; j++) occ = rdl(cell, j) == prop ? j : occ;
+            STAMP(13);
+            STAMP(14);
             const bool base = mover && !blocked;
-            for (int it = 0; it <= A; it++) {
-                const bool m = base && (occ < 0 || ((moved >> (occ & 63)) & 1ull));
-                const uint64_t nm = ballot(m);
-                if (nm == moved) break;
-                moved = nm;
+            if (!ballot(base && occ >= 0)) {
+                moved = ballot(base);  // nobody walks into an occupied cell: no chains to resolve
+            } else {
+                for (int it = 0; it <= A; it++) {
+                    const bool m = base && (occ < 0 || ((moved >> (occ & 63)) & 1ull));
+                    const uint64_t nm = ballot(m);
+                    if (nm == moved) break;
+                    moved = nm;
+                }
             }
+            STAMP(15);
             if ((moved >> lane) & 1ull) {
                 cell = prop;
                 if (!(MDL_ABLATE & 16)) vmask = p.movevalid[mgoff + cell_r(cell) * mW + cell_c(cell)];  // consumed at write-back
@@ -581,13 +617,13 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             s = s + ((!moved_a && mv == MV_S && pcarry == 0 && idle) ? cs[SH_IDLE] : 0.0f);
             s_lane = act ? s : 0.0f;
         }
-        const float shaped = (float)rr + np_sum_lanes(s_lane, A);
+        const float shaped = (float)rr + (SMALL ? np_sum_lanes8(s_lane, A) : np_sum_lanes(s_lane, A));
 
         STAMP(9);
         // ---- tracker update with the new state; a done env that resets here skips
         // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
         const bool do_rst = done && auto_reset;
-        if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, carry, t1);
+        if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH, SMALL>(ps, td, dirty, pk, P, A, carry, t1);
 
         // ---- reset on done (MAPPO/trainer.py:230-235) ----
         int t_out = t1;
@@ -608,7 +644,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
                 pk[c] = j < P ? L.pk[j] : 0;
                 ps[c] = (j < P ? L.pst[j] : 0u) | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
             }
-            if (STALE) tracker_update_regs<NCH>(ps, td, dirty, pk, P, A, 0, 0);
+            if (STALE) tracker_update_regs<NCH, SMALL>(ps, td, dirty, pk, P, A, 0, 0);
             t_out = 0;
             total_out = 0.0;
             any_rst = true;
@@ -647,7 +683,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
     STAMP(11);
 #ifdef MDL_STAMPS
     if (lane == 0)
-        for (int k = 0; k < 12; k++) g_stamps[(size_t)w * 16 + k] = stamp_[k];
+        for (int k = 0; k < 16; k++) g_stamps[(size_t)w * 16 + k] = stamp_[k];
 #endif
 }
 
@@ -1066,12 +1102,16 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
                           double* r, float* sh, uint8_t* done, int wpb, size_t lds, int K, hipStream_t s) {
 #ifdef MDL_STEP_WPB  // profiling builds only: workgroup shape experiments
     wpb = MDL_STEP_WPB;
-    hipLaunchKernelGGL((k_step<ST, NCH, FUSED>), dim3(blocks_for(n, wpb)), dim3(64 * wpb), lds * wpb, s, p, actions,
-                       fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+    const int threads = 64 * wpb;
 #else
-    hipLaunchKernelGGL((k_step<ST, NCH, FUSED>), dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, actions, fmt,
-                       ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+    const int threads = 256;
 #endif
+    if (p.A <= 8)
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, true>), dim3(blocks_for(n, wpb)), dim3(threads), lds * wpb, s, p,
+                           actions, fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+    else
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, false>), dim3(blocks_for(n, wpb)), dim3(threads), lds * wpb, s, p,
+                           actions, fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
 }
 
 template <bool ST, bool FUSED>

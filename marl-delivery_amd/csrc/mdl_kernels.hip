@@ -110,26 +110,29 @@ __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[N
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
-        if (j < P && pk_st(pk[c]) == t && !(ps[c] & PS_PRESENT)) {
-            ps[c] = (ps[c] & PS_STATUS) | PS_PRESENT;
-            td[c] = pk[c];
-            dirty[c] = true;
-        }
+        // selects, not branches: a branch here costs a vector-to-scalar hand-off
+        const bool ins = (j < P) & (pk_st(pk[c]) == t) & !(ps[c] & PS_PRESENT);
+        ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
+        td[c] = ins ? pk[c] : td[c];
+        dirty[c] = dirty[c] || ins;
     }
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int id = c * WAVE + lane + 1;
         bool carried = false;
         if constexpr (SMALL) {  // A <= 8: lanes >= A carry 0 and ids start at 1, so no bound is needed
+            uint32_t ci[8], mn = 0xffffffffu;  // min of (carry_i ^ id): zero iff some robot carries id
 #pragma unroll
-            for (int i = 0; i < 8; i++) carried |= rdl(carry, i) == id;
+            for (int i = 0; i < 8; i++) ci[i] = (uint32_t)rdl(carry, i);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 8; i++) mn = min(mn, ci[i] ^ (uint32_t)id);
+            carried = mn == 0u;
         } else {
             for (int i = 0; i < A; i++) carried |= rdl(carry, i) == id;
         }
-        if (ps[c] & PS_PRESENT) {
-            if (carried) ps[c] |= PS_TRANSIT;
-            else if (ps[c] & PS_TRANSIT) ps[c] &= PS_STATUS;
-        }
+        const uint32_t upd = carried ? (ps[c] | PS_TRANSIT) : (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
+        ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
     }
 }
 
@@ -397,26 +400,36 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             // now standing on the proposed cell (robots stand on distinct cells)
             int blocked = 0, occ = -1;
             if constexpr (SMALL) {
-                // Every test is one compare of this lane's proposal against a scalar, and the
-                // per-j answers combine as wave masks in scalar registers (no lane-serial chain):
-                //   blocked: lanes above j where mover j proposes the same cell
-                //   occ:     the (unique) robot j standing on the proposed cell, as 3 bits
-                const uint32_t mv32 = (uint32_t)movers;
-                uint64_t bl = 0, has = 0, o0 = 0, o1 = 0, o2 = 0;
+                // Every test is one compare of this lane's proposal against a readlane'd
+                // scalar, folded into vector registers (hit bits / occupant index): the
+                // chain never hands a vector result to the scalar unit, whose forwarding
+                // latency (~20 cycles per hand-off) would otherwise set the pace.
+                // Lanes >= A read as sentinels that match no cell.
+                const int propx = act ? prop : -2, cellx = act ? cell : -3;
+                // Three phases kept apart so no instruction waits on the one before it:
+                // all readlanes, all compares, then the selects.
+                int pj[8], cj[8];
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
-                    const uint64_t above = ((mv32 >> j) & 1u) ? (~0ull << (j + 1)) : 0ull;
-                    bl |= ballot(rdl(prop, j) == prop) & above;
-                    const uint64_t m = ballot(rdl(cell, j) == prop) & (j < A ? ~0ull : 0ull);
-                    has |= m;
-                    if (j & 1) o0 |= m;
-                    if (j & 2) o1 |= m;
-                    if (j & 4) o2 |= m;
+                    pj[j] = rdl(propx, j);
+                    cj[j] = rdl(cellx, j);
                 }
-                blocked = (int)((bl >> lane) & 1ull);
-                occ = ((has >> lane) & 1ull) ? (int)(((o0 >> lane) & 1ull) | (((o1 >> lane) & 1ull) << 1) |
-                                                     (((o2 >> lane) & 1ull) << 2))
-                                             : -1;
+                __builtin_amdgcn_sched_barrier(0);
+                bool hj[8], oj[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    hj[j] = pj[j] == prop;
+                    oj[j] = cj[j] == prop;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                uint32_t hit = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    hit |= hj[j] ? (1u << j) : 0u;
+                    occ = oj[j] ? j : occ;
+                }
+                // a lower-index mover into the same cell (only lanes < A are movers)
+                blocked = (hit & ((1u << (lane & 7)) - 1u) & (uint32_t)movers) != 0u;
             } else {
                 for (uint64_t m = movers; m; m &= m - 1) {
                     const int j = ffs64(m);

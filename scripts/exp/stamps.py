@@ -33,6 +33,12 @@ for E in [int(x) for x in (sys.argv[1:] or ["1024", "4096"])]:
     assert _lib.lib().mdl_debug_stamps(C.c_void_p(buf.ctypes.data), C.c_size_t(buf.nbytes)) == 0
     st = buf[:E, :12].astype(np.int64)
     d = np.diff(st, axis=1)
+    mv = buf[:E, [3, 12, 13, 14, 15, 4]].astype(np.int64)
+    if os.environ.get("MOVE_DETAIL"):
+        md = np.diff(mv, axis=1)
+        ok = (mv[:, 1:5] != 0).all(1)   # envs that had movers (inner stamps ran)
+        print("move detail (prop, movers loop, occ loop, fixed point, tail):",
+              [float(np.median(md[ok, i])) for i in range(5)], "envs", int(ok.sum()), file=sys.stderr)
     res[E] = {
         "median_cycles": {n: float(np.median(d[:, i])) for i, n in enumerate(names)},
         "p90_cycles": {n: float(np.percentile(d[:, i], 90)) for i, n in enumerate(names)},

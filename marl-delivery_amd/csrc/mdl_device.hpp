@@ -125,6 +125,22 @@ __device__ __forceinline__ float rdlf(float v, int j) {
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// lmask: a lane predicate as a 0 / ~0 word in a vector register, opaque to the
+// optimizer: predicates combined this way stay on the vector ALU.  Combined as
+// bools they become scalar lane masks, and every vector-compare -> scalar-op
+// hand-off costs ~20 cycles of forwarding latency (scripts/exp/probes.py).
+__device__ __forceinline__ uint32_t lmask(bool b) {
+    uint32_t x = b ? ~0u : 0u;
+    asm("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ uint32_t vbit(uint64_t m, int lane) { return 0u - (uint32_t)((m >> lane) & 1ull); }
+__device__ __forceinline__ float fmask(uint32_t m, float a) { return __uint_as_float(m & __float_as_uint(a)); }
+__device__ __forceinline__ float fpick(uint32_t m, float a, float b) {
+    return __uint_as_float((m & __float_as_uint(a)) | (~m & __float_as_uint(b)));
+}
+__device__ __forceinline__ int ipick(uint32_t m, int a, int b) { return (int)((m & (uint32_t)a) | (~m & (uint32_t)b)); }
+
 __device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 __device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((long long)m) - 1; }
 __device__ __forceinline__ uint64_t lanemask_lt() {

@@ -381,6 +381,27 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             }
         }
 
+        // The pre-step carried package of each robot, gathered from its package lane
+        // now (ds_bpermute) so the LDS round trip overlaps the movement: its table
+        // entry (drops), its tracker_prev entry and flags (shaped reward).
+        const int pj = carry - 1;
+        uint32_t g_pf = 0;
+        uint64_t g_td = 0, g_pk = 0;
+#pragma unroll
+        for (int c = 0; c < NCH && !(MDL_ABLATE & 64); c++) {
+            const int src = (pj & 63) << 2;
+            const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ps0[c]);
+            const uint32_t tlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)td[c]);
+            const uint32_t thi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(td[c] >> 32));
+            const uint32_t plo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)pk[c]);
+            const uint32_t phi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(pk[c] >> 32));
+            if ((pj >> 6) == c) {
+                g_pf = f;
+                g_td = (uint64_t)tlo | ((uint64_t)thi << 32);
+                g_pk = (uint64_t)plo | ((uint64_t)phi << 32);
+            }
+        }
+
         STAMP(3);
         // ---- movement (env.py:188-257) ----
         // moved = least fixed point of
@@ -439,13 +460,11 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             }
             STAMP(13);
             STAMP(14);
-            const bool base = mover && !blocked;
-            if (!ballot(base && occ >= 0)) {
-                moved = ballot(base);  // nobody walks into an occupied cell: no chains to resolve
-            } else {
-                for (int it = 0; it <= A; it++) {
-                    const bool m = base && (occ < 0 || ((moved >> (occ & 63)) & 1ull));
-                    const uint64_t nm = ballot(m);
+            const uint32_t Mbase = lmask(mover && !blocked), Mfree = lmask(occ < 0);
+            moved = ballot((Mbase & Mfree) != 0u);
+            if (ballot((Mbase & ~Mfree) != 0u)) {  // some walk into an occupied cell: resolve the chains
+                for (int it = 0; it < A; it++) {
+                    const uint64_t nm = ballot((Mbase & (Mfree | vbit(moved, occ & 63))) != 0u);
                     if (nm == moved) break;
                     moved = nm;
                 }
@@ -459,49 +478,47 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
         const int n_cost = popc64(moved);
 
         STAMP(4);
-        // ---- package actions (env.py:259-292); robots sit on distinct cells, so
-        // pick-ups and drops of different robots never interact ----
+        // ---- package actions (env.py:259-292) ----
+        // Robots sit on distinct cells, so pick-ups of different robots take from
+        // disjoint package sets and drops touch only carried packages: the robot
+        // order of the reference loop cannot change any outcome.
         uint64_t pickers = ballot(!(MDL_ABLATE & 8) && act && op == 1 && carry == 0);
-        while (pickers) {
-            const int i = ffs64(pickers);
-            pickers &= pickers - 1;
-            const int ci = rdl(cell, i);
-            int found = -1;
+        if (pickers) {
+            // per robot: the lowest-index waiting package at its cell
+            int sw[NCH];
+            uint64_t took[NCH];
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
-                if (found < 0) {
-                    const uint64_t b = ballot((ps[c] & PS_STATUS) == ST_WAITING && pk_start(pk[c]) == ci);
-                    if (b) {
-                        const int jj = ffs64(b);
-                        found = c * WAVE + jj;
-                        if (lane == jj) ps[c] = (ps[c] & ~PS_STATUS) | ST_IN_TRANSIT;
-                    }
-                }
+                sw[c] = (ps[c] & PS_STATUS) == ST_WAITING ? pk_start(pk[c]) : -2;  // unused lanes are ST_NONE
+                took[c] = 0;
             }
-            if (found >= 0 && lane == i) carry = found + 1;
+            int cnew = carry;
+            for (; pickers; pickers &= pickers - 1) {
+                const int i = ffs64(pickers);
+                const int ci = rdl(cell, i);
+                int fnd = -1;
+#pragma unroll
+                for (int c = 0; c < NCH; c++) {
+                    const uint64_t b = ballot(sw[c] == ci);
+                    took[c] |= fnd < 0 ? (b & (0ull - b)) : 0ull;
+                    fnd = (fnd < 0 && b != 0ull) ? c * WAVE + ffs64(b) : fnd;
+                }
+                cnew = lane == i ? fnd + 1 : cnew;  // not found: stays 0
+            }
+            carry = cnew;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) ps[c] = vbit(took[c], lane) ? ((ps[c] & ~PS_STATUS) | ST_IN_TRANSIT) : ps[c];
         }
-        uint64_t droppers = ballot(!(MDL_ABLATE & 8) && act && op == 2 && carry != 0);
-        uint64_t dmask = 0, omask = 0;
-        while (droppers) {
-            const int i = ffs64(droppers);
-            droppers &= droppers - 1;
-            const int j = rdl(carry, i) - 1;
-            const int ci = rdl(cell, i);
-            const int cc = j >> 6, jj = j & 63;
-            uint64_t v = 0;
+        // drops: a robot with op 2 carrying a package (its pre-step one: it did not
+        // pick) and standing on that package's target delivers it
+        const bool drop = !(MDL_ABLATE & 8) && act && op == 2 && carry != 0 && pk_target(g_pk) == cell;
+        const uint64_t dmask = ballot(drop), omask = ballot(drop && t0 <= pk_dl(g_pk));
+        carry = drop ? 0 : carry;
+        for (uint64_t m = dmask; m; m &= m - 1) {
+            const int j = rdl(pj, ffs64(m));
 #pragma unroll
             for (int c = 0; c < NCH; c++)
-                if (c == cc) v = pk[c];
-            const uint64_t d = (uint64_t)(uint32_t)rdl((int)(uint32_t)v, jj) |
-                               ((uint64_t)(uint32_t)rdl((int)(uint32_t)(v >> 32), jj) << 32);
-            if (pk_target(d) == ci) {
-                dmask |= 1ull << i;
-                if (t0 <= pk_dl(d)) omask |= 1ull << i;
-#pragma unroll
-                for (int c = 0; c < NCH; c++)
-                    if (c == cc && lane == jj) ps[c] = (ps[c] & ~PS_STATUS) | ST_DELIVERED;
-                if (lane == i) carry = 0;
-            }
+                ps[c] = (c * WAVE + lane == j) ? ((ps[c] & ~PS_STATUS) | ST_DELIVERED) : ps[c];
         }
         // reward: fp64 fold in the reference's order (move costs, then deliveries)
         double rr = 0.0;
@@ -533,28 +550,20 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
         // (s starts at +0 and never becomes -0).
         float s_lane = 0.0f;
         if (!(MDL_ABLATE & 1)) {
-            // tracker_prev entry of each agent's previously carried id (ds_bpermute gather)
-            const int pj = pcarry - 1;
-            uint32_t pf = 0;
-            uint64_t pdat = 0;
-#pragma unroll
-            for (int c = 0; c < NCH && !(MDL_ABLATE & 64); c++) {
-                const int src = (pj & 63) << 2;
-                const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ps0[c]);
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)td[c]);
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(td[c] >> 32));
-                if ((pj >> 6) == c) {
-                    pf = f;
-                    pdat = (uint64_t)lo | ((uint64_t)hi << 32);
-                }
-            }
-            const bool ppres = act && pcarry != 0 && pcarry <= P &&
-                               (STALE ? (pf & PS_PRESENT) != 0
-                                      : ((pf & PS_STATUS) == ST_WAITING || (pf & PS_STATUS) == ST_IN_TRANSIT));
-            const bool moved_a = pcell != cell;
-            const bool need_near = act && moved_a && !(pcarry != 0 && ppres);
-            const bool need_idle = act && !moved_a && mv == MV_S && pcarry == 0;
-            const bool need_can = act && op == 1 && pcarry == 0 && carry == 0;
+            // tracker_prev entry of each agent's previously carried id (gathered above)
+            const uint32_t pf = g_pf;
+            const uint64_t pdat = g_td;
+            // Lane predicates as vector masks (lmask): combined on the vector ALU.
+            const uint32_t Mact = lmask(act), Mpc0 = lmask(pcarry == 0), Mc0 = lmask(carry == 0);
+            const uint32_t Mpres =
+                Mact & ~Mpc0 & lmask(pcarry <= P) &
+                (STALE ? lmask((pf & PS_PRESENT) != 0)
+                       : lmask((pf & PS_STATUS) == ST_WAITING) | lmask((pf & PS_STATUS) == ST_IN_TRANSIT));
+            const uint32_t Mmov = lmask(pcell != cell), MS = lmask(mv == MV_S);
+            const uint32_t Mop1 = lmask(op == 1), Mop2 = lmask(op == 2);
+            const bool need_near = (Mact & Mmov & (Mpc0 | ~Mpres)) != 0u;
+            const bool need_idle = (Mact & ~Mmov & MS & Mpc0) != 0u;
+            const bool need_can = (Mact & Mop1 & Mpc0 & Mc0) != 0u;
             bool wv[NCH];
             int stc[NCH];
             uint64_t anyw = 0;
@@ -602,33 +611,43 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
                     can_m |= (uint64_t)(h != 0) << a;
                 }
             }
-            const bool idle = (idle_m >> lane) & 1ull, can = (can_m >> lane) & 1ull;
+            const uint32_t Midle = vbit(idle_m, lane), Mcan = vbit(can_m, lane);
             STAMP(8);
-            // the constants, pinned in SGPRs so the selects below stay branch-free
+            // the constants, pinned in SGPRs
             float cs[9];
 #pragma unroll
             for (int k = 0; k < 9; k++) {
                 cs[k] = p.shaping[k];
                 pin(cs[k]);
             }
+            // The reference's if-chains, term by term.  Each term is a masked constant
+            // (+0.0f when no branch fires; the alternatives within a term are disjoint).
             const int ptg = pk_target(pdat);
-            float s = 0.0f;
+            const uint32_t Mtg = lmask(cell == ptg);
             // 1. pickup / delivery
-            const bool pick = pcarry == 0 && carry != 0;
-            const bool deliv = pcarry != 0 && carry == 0 && ppres && cell == ptg;
-            s = s + (pick ? cs[SH_PICK] : deliv ? ((t1 <= pk_dl(pdat)) ? cs[SH_ONTIME] : cs[SH_LATE]) : 0.0f);
+            const uint32_t Mpick = Mpc0 & ~Mc0;
+            const uint32_t Mdeliv = ~Mpc0 & Mc0 & Mpres & Mtg;
+            const float t1v = fmask(Mpick, cs[SH_PICK]) +
+                              fmask(Mdeliv, fpick(lmask(t1 <= pk_dl(pdat)), cs[SH_ONTIME], cs[SH_LATE]));
             // 2. wasted operations
-            const bool wpick = op == 1 && (pcarry != 0 || (carry == 0 && !can));
-            const bool wdrop = op == 2 && (pcarry == 0 || (carry != 0 && ppres && cell != ptg));
-            s = s + (wpick ? cs[SH_WPICK] : wdrop ? cs[SH_WDROP] : 0.0f);
+            const uint32_t Mwpick = Mop1 & (~Mpc0 | (Mc0 & ~Mcan));
+            const uint32_t Mwdrop = Mop2 & (Mpc0 | (~Mc0 & Mpres & ~Mtg));
+            const float t2v = fmask(Mwpick, cs[SH_WPICK]) + fmask(Mwdrop, cs[SH_WDROP]);
             // 3. movement
-            s = s + ((mv != MV_S && !moved_a) ? cs[SH_STUCK] : 0.0f);
-            const int tgt = (pcarry != 0 && ppres) ? ptg : best_cell;
+            const float t3v = fmask(~MS & ~Mmov, cs[SH_STUCK]);
+            const int tgt = ipick(~Mpc0 & Mpres, ptg, best_cell);
             const int db = manhattan(pcell, tgt), da = manhattan(cell, tgt);
-            s = s + ((tgt >= 0 && moved_a) ? (da < db ? cs[SH_CLOSER] : da > db ? cs[SH_AWAY] : 0.0f) : 0.0f);
+            const uint32_t Mt = lmask(tgt >= 0) & Mmov;
+            const float t4v = fmask(Mt & lmask(da < db), cs[SH_CLOSER]) + fmask(Mt & lmask(da > db), cs[SH_AWAY]);
             // 4. idle next to an available package
-            s = s + ((!moved_a && mv == MV_S && pcarry == 0 && idle) ? cs[SH_IDLE] : 0.0f);
-            s_lane = act ? s : 0.0f;
+            const float t5v = fmask(~Mmov & MS & Mpc0 & Midle, cs[SH_IDLE]);
+            float s = 0.0f;
+            s = s + t1v;
+            s = s + t2v;
+            s = s + t3v;
+            s = s + t4v;
+            s = s + t5v;
+            s_lane = fmask(Mact, s);
         }
         const float shaped = (float)rr + (SMALL ? np_sum_lanes8(s_lane, A) : np_sum_lanes(s_lane, A));
 

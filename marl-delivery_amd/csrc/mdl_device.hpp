@@ -83,6 +83,10 @@ struct DevParams {
     uint64_t* trk;             // [E][P] stale mode: a tracker entry's data (written at insertion)
     double* ep_total;          // [E] total_reward of the last finished episode
     int32_t* ep_len;           // [E]
+    // observation builders (appended: the step kernel's argument layout stays put)
+    const double* obs_recip;   // [2 * n_maps + 2]: 1/H, 1/W of each map, then 1/obsT, 1/(MR-1), fp64 RN
+    int obs_plane_words;       // > 0: k_obs stages the map planes as bit words (LDS words reserved per wave)
+    int obs_small;             // k_obs_small builds the observations (mdl_obs_small.hpp)
 };
 
 // Robot word: bits 0-15 cell (r | c<<8), bits 16-26 carried package id,
@@ -163,6 +167,15 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x143, 0xc, 0xf, false); v = t < v ? t : v;  // row_bcast:31
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+
+// float32(a / b) for an int a and an int b > 0 whose fp64 reciprocal y = RN(1/b)
+// is precomputed: RN_f32(RN_f64(a * y)).  Exact (== qdiv) for |a| < 2^24,
+// b < 2^24: a*y is within 2^-52 (relative) of a/b, while a/b is either a float
+// or at least 2^-49 (relative) away from every float32 rounding boundary
+// (a/b = midpoint would need a 25-bit odd significand from a 24-bit a).
+// For |a| >= 2^24 it is float32(float64(a)/b), which is what the reference's
+// Python-float division followed by the float32 cast computes.
+__device__ __forceinline__ float qdiv_r(int a, double y) { return (float)((double)a * y); }
 
 // Correctly rounded int/int division in float32.  For |a|,|b| < 2^24 this
 // equals float32(double(a)/double(b)) (double rounding is innocuous for

@@ -284,6 +284,16 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     rc |= eng->alloc(&d_bits, allbits.size());
     rc |= eng->alloc(&d_free, allfree.size());
     rc |= eng->alloc(&d_rank, allrank.size());
+    // fp64 reciprocals for the observation builders' divisions (qdiv_r)
+    std::vector<double> recip;
+    for (int m = 0; m < n_maps; m++) {
+        recip.push_back(1.0 / (double)eng->mapH[m]);
+        recip.push_back(1.0 / (double)eng->mapW[m]);
+    }
+    recip.push_back(c.obs_max_time_steps > 0 ? 1.0 / (double)c.obs_max_time_steps : 0.0);
+    recip.push_back(c.max_robots_state > 1 ? 1.0 / (double)(c.max_robots_state - 1) : 0.0);
+    double* d_recip = nullptr;
+    rc |= eng->alloc(&d_recip, recip.size());
     if (env_map) rc |= eng->alloc(&d_em, E);
     rc |= eng->alloc(&p.rob, E * A);
     rc |= eng->alloc(&p.pkg, E * P);
@@ -304,6 +314,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         hipMemcpy(d_bits, allbits.data(), allbits.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_free, allfree.data(), allfree.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_rank, allrank.data(), allrank.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_recip, recip.data(), recip.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
         (env_map && hipMemcpy(d_em, em.data(), E, hipMemcpyHostToDevice) != hipSuccess)) {
         delete eng;
         return fail("hipMemcpy of map tables failed");
@@ -313,6 +324,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     p.gridbits = d_bits;
     p.free_cells = d_free;
     p.rank = d_rank;
+    p.obs_recip = d_recip;
     p.env_map = d_em;
     {
         uint64_t h = 1469598103934665603ull;
@@ -330,7 +342,10 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
 
     eng->lds_step = mdl::step_lds((int)P);
     eng->wpb_step = waves_per_block(eng->lds_step);
-    eng->lds_obs = mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MO, p.MP, p.MR, p.MPs);
+    p.obs_plane_words = mdl::obs_plane_words((int)A, eng->maxHW);
+    p.obs_small = mdl::obs_use_small((int)A, (int)P, p.MO, p.MP, p.key32_dsh, eng->maxHW) && !getenv("MDL_OBS_GENERIC");
+    eng->lds_obs = p.obs_small ? mdl::obs_lds_small((int)A, eng->maxHW)
+                               : mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MO, p.MP, p.MR, p.MPs);
     eng->wpb_obs = waves_per_block(eng->lds_obs);
     if (eng->wpb_step < 1 || eng->wpb_obs < 1) {
         delete eng;

@@ -370,6 +370,61 @@ __device__ __forceinline__ uint32_t actor_bits4(const FeatLds& L, int NW, int a,
     return wb;
 }
 
+// ---- map outputs from plane words (engine path) ----
+// Every output map plane as bit words in LDS: actor plane (a, ch) at word
+// (6a + ch) * NW, critic plane ch at (6A + ch) * NW.  Each float4 of the
+// outputs is then one LDS word, a shift and four selects.
+__host__ __device__ inline int plane_words(int A, int HW) { return (6 * A + 4) * ((HW + 31) / 32); }
+
+__device__ inline void feat_build_planes(const FeatCtx& c, const FeatLds& L, uint32_t* pl) {
+    const int lane = lane_id();
+    const int NW = c.NW, A = c.A, n = (6 * A + 4) * NW;
+    const float inv_nw = 1.0f / (float)NW;
+    for (int k = lane; k < n; k += WAVE) {
+        const int p = fdivi(k, NW, inv_nw);
+        const int w = k - p * NW;
+        const int base = w << 5;
+        const uint32_t g = L.bits[BS_GRID * NW + w], rb = L.bits[BS_ROBOT * NW + w];
+        const uint32_t ws = L.bits[BS_WSTART * NW + w], at = L.bits[BS_ATARGET * NW + w];
+        uint32_t v;
+        if (p < 6 * A) {
+            const int a = p / 6, ch = p - 6 * a;
+            const unsigned od = (unsigned)(L.rcell[a] - base), td = (unsigned)(L.rtgt[a] - base);
+            const uint32_t ow = od < 32u ? 1u << od : 0u;
+            const uint32_t tw = td < 32u ? 1u << td : 0u;   // rtgt = -1: no bit
+            const uint32_t oth = (rb & ~ow) | L.bits[BS_MULTI * NW + w];
+            v = ch == 0 ? g : ch == 1 ? ow : ch == 2 ? oth : ch == 3 ? ws : ch == 4 ? at : tw;
+        } else {
+            const int ch = p - 6 * A;
+            v = ch == 0 ? g : ch == 1 ? rb : ch == 2 ? ws : at;
+        }
+        pl[k] = v;
+    }
+    wave_sync();
+}
+
+// Planes [0, np) of pl (HW cells each, HW % 4 == 0) as float4 rows into dst
+// (16-B aligned).  The (plane, float4-in-plane) pair of each lane advances by
+// a constant per iteration: no division in the loop.
+__device__ inline void emit_planes(const uint32_t* pl, int NW, int np, int HW, float* dst) {
+    const int lane = lane_id();
+    const int qpp = HW >> 2, nq = np * qpp;
+    const int dp = WAVE / qpp, dr = WAVE - dp * qpp;
+    int p = lane / qpp;
+    int r = lane - p * qpp;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int q = lane; q < nq; q += WAVE) {
+        const int c0 = r << 2;
+        d4[q] = float4_of_bits((pl[p * NW + (c0 >> 5)] >> (c0 & 31)) & 15u);
+        p += dp;
+        r += dr;
+        if (r >= qpp) {
+            r -= qpp;
+            p += 1;
+        }
+    }
+}
+
 // convert_observation for agents [a0, a0+na): dst [na][6][H][W].
 // a_valid=false reproduces the early return (channel 0 only).
 __device__ inline void emit_actor_maps(const FeatCtx& c, const FeatLds& L, int a0, int na, bool a_valid, float* dst) {

@@ -19,6 +19,7 @@
 // readlane / ballot only; LDS is touched only when an env resets.
 #include "mdl_kernels.hpp"
 #include "mdl_features.hpp"
+#include "mdl_obs_small.hpp"
 #include "mdl_altfeat.hpp"
 
 // Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
@@ -767,6 +768,10 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
     c.inv_hw = md.inv_hw;
     FeatDims fd{A, P, c.HW, c.MPc, c.MPsc, stage_floats(A, A, c.MO, c.MPc, c.MR, c.MPsc)};
     FeatLds L = feat_carve(base + obs_pre_bytes(P), fd);
+    // plane words: reserved for the largest map; HW % 4 == 0 maps use them
+    uint32_t* planes = (p.obs_plane_words > 0 && (c.HW & 3) == 0)
+                           ? (uint32_t*)(base + obs_pre_bytes(P) + feat_lds_bytes(fd))
+                           : nullptr;
 
     const bool act = lane < A;
     const uint32_t rv = act ? p.rob[(size_t)e * A + lane] : 0u;
@@ -788,8 +793,16 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
     auto run = [&](const auto& trk) {
         feat_prepare(trk, c, L, cell, carry);
         const size_t le = (size_t)w;
-        if (amap) emit_actor_maps(c, L, 0, A, true, amap + le * (size_t)A * 6 * c.HW);
-        if (cmap) emit_critic_map(c, L, cmap + le * 4 * (size_t)c.HW);
+        float* am = amap ? amap + le * (size_t)A * 6 * c.HW : nullptr;
+        float* cm = cmap ? cmap + le * 4 * (size_t)c.HW : nullptr;
+        if (planes && (((uintptr_t)am | (uintptr_t)cm) & 15) == 0 && (am || cm)) {
+            feat_build_planes(c, L, planes);
+            if (am) emit_planes(planes, c.NW, 6 * A, c.HW, am);
+            if (cm) emit_planes(planes + 6 * A * c.NW, c.NW, 4, c.HW, cm);
+        } else {
+            if (am) emit_actor_maps(c, L, 0, A, true, am);
+            if (cm) emit_critic_map(c, L, cm);
+        }
         if (avec) {
             if (p.key32_dsh > 0 && P <= WAVE && A <= 8) {
                 for (int a = 0; a < A; a++) feat_sort_others(c, L, a, cell);
@@ -1206,6 +1219,15 @@ hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt
 
 hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
                       int wpb, size_t lds, hipStream_t s) {
+    if (p.obs_small) {
+        if (p.stale)
+            hipLaunchKernelGGL(k_obs_small<true>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin, n,
+                               amap, avec, cmap, cvec, wpb, (int)lds);
+        else
+            hipLaunchKernelGGL(k_obs_small<false>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin,
+                               n, amap, avec, cmap, cvec, wpb, (int)lds);
+        return hipGetLastError();
+    }
     if (p.stale)
         hipLaunchKernelGGL(k_obs<true>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin, n, amap,
                            avec, cmap, cvec, wpb, (int)lds);
@@ -1241,10 +1263,18 @@ hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int
 }
 
 size_t step_lds(int P) { return reset_lds_bytes(P); }
+size_t obs_lds_small(int A, int HW) { return obs_small_lds(A, HW); }
+bool obs_use_small(int A, int P, int MO, int MP, int key32_dsh, int maxHW) {
+    return obs_small_ok(A, P, MO, MP, key32_dsh, maxHW);
+}
 size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs) {
     const int MPc = MP < P ? MP : P, MPsc = MPs < P ? MPs : P;
     FeatDims d{A, P, HW, MPc, MPsc, stage_floats(A, A, MO, MPc, MR, MPsc)};
-    return obs_pre_bytes(P) + feat_lds_bytes(d);
+    return obs_pre_bytes(P) + feat_lds_bytes(d) + 4 * (size_t)obs_plane_words(A, HW);
+}
+int obs_plane_words(int A, int HW) {
+    const int w = plane_words(A, HW);
+    return w <= 2048 ? w : 0;   // larger maps (64x64) keep the per-float4 bitset path
 }
 size_t views_lds(int NSmax, int HW, int MO, int MPc, int MR, int MPsc) {
     FeatDims d{64, NSmax, HW, MPc, MPsc, stage_floats(64, 1, MO, MPc, MR, MPsc)};

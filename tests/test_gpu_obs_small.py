@@ -1,0 +1,101 @@
+"""k_obs_small (csrc/mdl_obs_small.hpp) vs the generic k_obs builder and the
+oracle: the engine's fast observation path for A <= 8, P <= 64, <= 8 package
+slots must produce the same bits as the generic path for every output
+(MAPPO/helper.py:6-255) on identical states, across maps (HW % 4 == 0 and
+not), both tracker modes, padded and unpadded vector layouts, MR < A, and
+obs_max_time_steps <= 0."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from golden_io import grid
+
+pytestmark = pytest.mark.gpu
+
+
+def _mg():
+    import marl_gpu
+    return marl_gpu
+
+
+def _pair(mg, g, E, A, P, T, **kw):
+    """Two engines with identical streams: the small builder and (MDL_OBS_GENERIC) the generic one."""
+    a = mg.BatchedEnv(g, E, A, P, T, **kw)
+    os.environ["MDL_OBS_GENERIC"] = "1"
+    try:
+        b = mg.BatchedEnv(g, E, A, P, T, **kw)
+    finally:
+        del os.environ["MDL_OBS_GENERIC"]
+    return a, b
+
+
+CASES = [
+    # map, A, P, T, tracker, MO, MP, MR, MPs, obsT
+    ("map1.txt", 5, 50, 60, "mappo", 4, 5, 100, 100, None),      # config 3 sizes (MAPPO trainer)
+    ("map1.txt", 5, 50, 60, "fresh", 4, 5, 10, 20, None),        # QMIX config sizes
+    ("map.txt", 4, 20, 30, "mappo", 6, 8, 3, 10, None),          # 7x7 (HW % 4 != 0), padded others, MR < A
+    ("map2.txt", 3, 64, 40, "fresh", 2, 8, 100, 30, 0),          # P = 64, obsT = 0
+    ("map3.txt", 7, 30, 25, "mappo", 6, 1, 8, 30, 17),           # A = 7 (63 tuple lanes), one package slot, obsT < T
+    ("map1.txt", 1, 10, 20, "mappo", 0, 3, 1, 5, None),          # one robot
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-A{c[1]}-P{c[2]}-{c[4]}" for c in CASES])
+def test_small_builder_matches_generic(case):
+    mg = _mg()
+    m, A, P, T, tracker, MO, MP, MR, MPs, obsT = case
+    g = grid(m)
+    E = 96
+    kw = dict(seed=11, tracker=tracker, max_other_robots=MO, max_packages_obs=MP, max_robots_state=MR,
+              max_packages_state=MPs, obs_max_time_steps=obsT)
+    a, b = _pair(mg, g, E, A, P, T, **kw)
+    a.reset()
+    b.reset()
+    gen = np.random.RandomState(5)
+    for k in range(2 * T + 7):
+        acts = torch.from_numpy(gen.randint(0, 15, size=(E, A)).astype(np.uint8)).cuda()
+        a.step(acts)
+        b.step(acts)
+        if k % 9 == 4:
+            oa, ob = a.build_obs(), b.build_obs()
+            for key in ("actor_map", "actor_vec", "critic_map", "critic_vec"):
+                x, y = oa[key].cpu().numpy(), ob[key].cpu().numpy()
+                assert x.shape == y.shape
+                # bitwise (also the sign of zeros)
+                assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (key, k)
+    a.close()
+    b.close()
+
+
+def test_small_builder_config3_vs_oracle():
+    """Config 3 featurizer sizes along a MAPPO rollout (stale tracker, auto-reset), checked
+    against the oracle's literal restatement of the three helpers."""
+    mg = _mg()
+    g = grid("map1.txt")
+    E, A, P, T = 16, 5, 50, 40
+    env = mg.BatchedEnv(g, E, A, P, T, seed=42, tracker="mappo", max_other_robots=4, max_packages_obs=5)
+    env.reset()
+    ob = O.OracleBatch(E, g, A, P, T, seed_base=42, clear_on_reset=False)
+    gen = np.random.RandomState(3)
+    for k in range(90):
+        ints = gen.randint(0, 15, size=(E, A)).astype(np.uint8)
+        env.step(torch.from_numpy(ints).cuda())
+        ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS)
+        if k % 15 == 7:
+            o = env.build_obs()
+            av, cv = o["actor_vec"].cpu().numpy(), o["critic_vec"].cpu().numpy()
+            am, cm = o["actor_map"].cpu().numpy(), o["critic_map"].cpu().numpy()
+            for e in range(E):
+                oe, ot = ob.env(e), ob.tracker(e)
+                st, rb1, rows = oe.state(), oe.robots1(), ot.rows()
+                for a in range(A):
+                    np.testing.assert_array_equal(
+                        av[e, a], O.generate_vector_features(10, 10, st["t"], rb1, rows, a, T, 4, 5))
+                    np.testing.assert_array_equal(am[e, a], O.convert_observation(g, st["t"], rb1, rows, a))
+                gm, gv = O.convert_global_state(g, st["t"], rb1, rows, T, 100, 100)
+                np.testing.assert_array_equal(cv[e], gv)
+                np.testing.assert_array_equal(cm[e], gm)
+    env.close()

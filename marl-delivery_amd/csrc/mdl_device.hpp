@@ -87,6 +87,7 @@ struct DevParams {
     const double* obs_recip;   // [2 * n_maps + 2]: 1/H, 1/W of each map, then 1/obsT, 1/(MR-1), fp64 RN
     int obs_plane_words;       // > 0: k_obs stages the map planes as bit words (LDS words reserved per wave)
     int obs_small;             // k_obs_small builds the observations (mdl_obs_small.hpp)
+    int key7_dsh;              // > 0: (max(0,dl-t), rank, 7-bit order) fits 32 bits, dlc at this shift
 };
 
 // Robot word: bits 0-15 cell (r | c<<8), bits 16-26 carried package id,

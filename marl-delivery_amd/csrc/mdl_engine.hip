@@ -271,6 +271,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         auto bits = [](long v) { int b = 0; while (v > 0) { b++; v >>= 1; } return b; };
         const int rb = bits(rank_max), db = bits(dl_max);
         p.key32_dsh = (11 + rb + db <= 32) ? 11 + rb : 0;
+        p.key7_dsh = (7 + rb + db <= 32) ? 7 + rb : 0;
     }
 
     const size_t E = c.n_envs, A = c.n_robots, P = c.n_packages;
@@ -343,10 +344,14 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     eng->lds_step = mdl::step_lds((int)P);
     eng->wpb_step = waves_per_block(eng->lds_step);
     p.obs_plane_words = mdl::obs_plane_words((int)A, eng->maxHW);
-    p.obs_small = mdl::obs_use_small((int)A, (int)P, p.MO, p.MP, p.key32_dsh, eng->maxHW) && !getenv("MDL_OBS_GENERIC");
+    p.obs_small = mdl::obs_use_small((int)A, (int)P, p.key7_dsh, eng->maxHW) && !getenv("MDL_OBS_GENERIC");
     eng->lds_obs = p.obs_small ? mdl::obs_lds_small((int)A, eng->maxHW)
                                : mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MO, p.MP, p.MR, p.MPs);
     eng->wpb_obs = waves_per_block(eng->lds_obs);
+    if (const char* v = getenv("MDL_OBS_WPB")) {   // profiling override (1..4 waves per workgroup)
+        const int x = atoi(v);
+        if (x >= 1 && x < eng->wpb_obs) eng->wpb_obs = x;
+    }
     if (eng->wpb_step < 1 || eng->wpb_obs < 1) {
         delete eng;
         return fail("configuration needs more than %zu bytes of LDS per env", LDS_BUDGET);

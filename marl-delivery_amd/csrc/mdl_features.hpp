@@ -67,7 +67,8 @@ __device__ inline FeatLds feat_carve(unsigned char* base, const FeatDims& d) {
     return L;
 }
 
-enum : int { BS_GRID = 0, BS_ROBOT = 1, BS_MULTI = 2, BS_WSTART = 3, BS_ATARGET = 4 };
+// bitsets 0..3 are the critic map's planes in order (convert_global_state channels)
+enum : int { BS_GRID = 0, BS_ROBOT = 1, BS_WSTART = 2, BS_ATARGET = 3, BS_MULTI = 4 };
 
 struct FeatCtx {
     int A, NS, H, W, HW, NW, t, T, MO, MP, MR, MPs, MPc, MPsc;

@@ -1264,8 +1264,8 @@ hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int
 
 size_t step_lds(int P) { return reset_lds_bytes(P); }
 size_t obs_lds_small(int A, int HW) { return obs_small_lds(A, HW); }
-bool obs_use_small(int A, int P, int MO, int MP, int key32_dsh, int maxHW) {
-    return obs_small_ok(A, P, MO, MP, key32_dsh, maxHW);
+bool obs_use_small(int A, int P, int key7_dsh, int maxHW) {
+    return obs_small_ok(A, P, key7_dsh, maxHW);
 }
 size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs) {
     const int MPc = MP < P ? MP : P, MPsc = MPs < P ? MPs : P;

@@ -59,7 +59,7 @@ size_t step_lds(int P);
 size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs);
 int obs_plane_words(int A, int HW);
 size_t obs_lds_small(int A, int HW);
-bool obs_use_small(int A, int P, int MO, int MP, int key32_dsh, int maxHW);
+bool obs_use_small(int A, int P, int key7_dsh, int maxHW);
 size_t views_lds(int NSmax, int HW, int MO, int MPc, int MR, int MPsc);
 size_t views_shaped_lds(int NSmax);
 

@@ -1,16 +1,20 @@
 // mdl_obs_small.hpp -- the engine's observation builder for small envs:
-// A <= 8 robots, P <= 64 packages, <= 8 package slots per agent and 32-bit
-// package sort keys (the trainers' featurizer sizes: config 3 is map1, A = 5,
-// P = 50, MO = 4, MP = 5, MR = MPs = 100).  Same outputs as k_obs
-// (MAPPO/helper.py:6-255: convert_observation x A, generate_vector_features x A,
-// convert_global_state), built for VALU economy -- k_obs measured VALU-issue
-// bound (2.6k VALU instructions per env, 4 cycles each on a 16-lane SIMD):
+// A <= 8 robots, P <= 64 packages and 32-bit package sort keys (every trainer
+// configuration of the reference: config 3 is map1, A = 5, P = 50, MO = 4,
+// MP = 5, MR = MPs = 100; config 3b the helper defaults MO = MP = 100).
+// Same outputs as k_obs (MAPPO/helper.py:6-255: convert_observation x A,
+// generate_vector_features x A, convert_global_state), built for VALU economy --
+// k_obs measured VALU-issue bound (2.6k VALU instructions per env on config 3,
+// 4 cycles each on a 16-lane SIMD):
 //   * packages on lanes (lane j = slot j), robots on lanes (lane a = robot a);
-//     cross-lane data moves by ds_bpermute, never through per-value LDS tables;
-//   * every vector tuple (self / other robot / waiting package of an agent, a
-//     critic robot or package row) is computed by ONE lane in ONE uniform pass
-//     (the tuple kinds differ only in which operands feed the same five
-//     divisions), then stored straight to HBM; padding is a separate zero fill;
+//     cross-lane data moves by ds_bpermute / DPP, not through per-value tables;
+//   * package order per agent: repeated wave minima for a few slots, a bitonic
+//     sort of the 64 lanes otherwise;
+//   * every vector tuple (self / other robot / package slot of an agent, a
+//     critic robot or package row) is computed by ONE lane in uniform passes
+//     (the tuple kinds differ only in which operands feed the same divisions,
+//     each one fp64 multiply by a precomputed reciprocal) and stored straight to
+//     HBM; padding is a separate zero fill;
 //   * maps: every output plane as bit words in LDS, one float4 per word nibble.
 #pragma once
 #include "mdl_features.hpp"
@@ -20,6 +24,8 @@ namespace mdl {
 __device__ __forceinline__ int bperm(int v, int src_lane) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
 
 // n zeros at dst: dword head to 16-B alignment, float4 body, dword tail.
+// (Stores stay default-policy: nontemporal float4 stores measured slower,
+// config 3 actor maps alone 34 -> 47 us.)
 __device__ inline void zero_fill(float* dst, int n) {
     if (n <= 0) return;
     const int lane = lane_id();
@@ -33,8 +39,8 @@ __device__ inline void zero_fill(float* dst, int n) {
     if (tail + lane < n) dst[tail + lane] = 0.0f;
 }
 
-// Planes [0, np) of pl (HW cells each) as floats at dst, one dword per cell
-// (maps with HW % 4 != 0 or an unaligned destination).
+// Planes [0, np) of pl (NW words each, HW cells) as floats at dst, one dword
+// per cell (maps with HW % 4 != 0 or an unaligned destination).
 __device__ inline void emit_planes_dword(const uint32_t* pl, int NW, int np, int HW, float* dst) {
     const int lane = lane_id();
     const float inv = 1.0f / (float)HW;
@@ -45,22 +51,78 @@ __device__ inline void emit_planes_dword(const uint32_t* pl, int NW, int np, int
     }
 }
 
-struct ObsSmallDims {
-    int A, NW;
-};
-// LDS bytes per wave: bitsets (5 NW words), planes ((6A+4) NW words), carrier
-// table (64 words), critic order (64 words), package selection (64 words).
-__host__ __device__ inline size_t obs_small_lds(int A, int HW) {
-    const int NW = (HW + 31) / 32;
-    return 4 * (size_t)((6 * A + 9) * NW) + 3 * 256;
+// Lane-mask select with the mask in an SGPR pair: bit l set -> b, else a (one VALU op).
+__device__ __forceinline__ uint32_t sel64(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
 }
 
-// Eligibility (host and device agree): see the file comment.
-__host__ __device__ inline bool obs_small_ok(int A, int P, int MO, int MP, int key32_dsh, int maxHW) {
-    const int MPc = MP < P ? MP : P;
-    const int MOc = MO < A - 1 ? MO : (A - 1 > 0 ? A - 1 : 0);
-    return A >= 1 && A <= 8 && P <= WAVE && MPc <= 8 && key32_dsh > 0 && A * (A + MPc + 1) <= WAVE &&
-           MOc >= 0 && obs_small_lds(A, maxHW) <= 16384;
+// The lanes that keep the maximum in bitonic step (K, J) (ascending network).
+template <int K, int J>
+__host__ __device__ constexpr uint64_t bitonic_max_lanes() {
+    uint64_t m = 0;
+    for (int l = 0; l < 64; l++)
+        if (((l & J) == 0) != ((l & K) == 0)) m |= 1ull << l;
+    return m;
+}
+
+// x of lane (lane ^ J): DPP for 1, 2, 8; ds_swizzle (bitmask mode) for 4, 16;
+// ds_bpermute for 32.
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
+    if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
+    else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false);   // 2,3,0,1
+    else if constexpr (J == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xf, 0xf, false);   // row_ror:8
+    else if constexpr (J == 4 || J == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1f | (J << 10));
+    else return (uint32_t)__builtin_amdgcn_ds_bpermute((lane_id() ^ J) << 2, (int)x);
+}
+
+template <int K, int J>
+__device__ __forceinline__ uint32_t bitonic_step(uint32_t x) {
+    const uint32_t y = xor_lane<J>(x);
+    const uint32_t mn = x < y ? x : y, mx = x < y ? y : x;
+    return sel64(bitonic_max_lanes<K, J>(), mn, mx);
+}
+
+// Ascending sort of one u32 per lane across the wave (bitonic network, 21 steps).
+__device__ inline uint32_t sort64_u32(uint32_t x) {
+    x = bitonic_step<2, 1>(x);
+    x = bitonic_step<4, 2>(x);
+    x = bitonic_step<4, 1>(x);
+    x = bitonic_step<8, 4>(x);
+    x = bitonic_step<8, 2>(x);
+    x = bitonic_step<8, 1>(x);
+    x = bitonic_step<16, 8>(x);
+    x = bitonic_step<16, 4>(x);
+    x = bitonic_step<16, 2>(x);
+    x = bitonic_step<16, 1>(x);
+    x = bitonic_step<32, 16>(x);
+    x = bitonic_step<32, 8>(x);
+    x = bitonic_step<32, 4>(x);
+    x = bitonic_step<32, 2>(x);
+    x = bitonic_step<32, 1>(x);
+    x = bitonic_step<64, 32>(x);
+    x = bitonic_step<64, 16>(x);
+    x = bitonic_step<64, 8>(x);
+    x = bitonic_step<64, 4>(x);
+    x = bitonic_step<64, 2>(x);
+    x = bitonic_step<64, 1>(x);
+    return x;
+}
+
+// LDS bytes per wave: bitsets (5 NW words), actor planes (6A NW words), carrier
+// table and critic order (64 words each), order -> slot map (128 B), package
+// order of each agent (8 x 64 B).
+__host__ __device__ inline size_t obs_small_lds(int A, int HW) {
+    const int NW = (HW + 31) / 32;
+    return 4 * (size_t)((6 * A + 5) * NW) + 2 * 256 + 128 + 512;
+}
+
+// Eligibility (host and device agree): A <= 8 robots, P <= 64 packages, the
+// package sort key (max(0,dl-t), rank, 7-bit order) in 32 bits, LDS slice <= 16 KiB.
+__host__ __device__ inline bool obs_small_ok(int A, int P, int key7_dsh, int maxHW) {
+    return A >= 1 && A <= 8 && P >= 1 && P <= WAVE && key7_dsh > 0 && obs_small_lds(A, maxHW) <= 16384;
 }
 
 template <bool STALE>
@@ -74,22 +136,23 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
     if (wave >= wpb || w >= n) return;
     const int e = env_begin + w;
     const int A = p.A, P = p.P;
-    const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
+    const int mi = p.env_map ? p.env_map[e] : 0;
+    const MapDesc md = p.maps[mi];
     const int H = md.H, W = md.W, HW = H * W, NW = (HW + 31) / 32;
     const int T = p.obsT, MO = p.MO, MP = p.MP, MR = p.MR, MPs = p.MPs;
     const int MPc = MP < P ? MP : P, MPsc = MPs < P ? MPs : P;
     const int MOc = MO < A - 1 ? MO : A - 1;
-    const int mi = p.env_map ? p.env_map[e] : 0;
     const double yH = p.obs_recip[2 * mi], yW = p.obs_recip[2 * mi + 1];   // RN(1/H), RN(1/W)
     const double yT = p.obs_recip[2 * p.n_maps], yM = p.obs_recip[2 * p.n_maps + 1];
     const uint16_t* rank = p.rank + md.rank_off;
     const int rW = 2 * W - 1, rOff = (H - 1) * rW + (W - 1);   // rank[(dr+H-1)*(2W-1) + dc+W-1]
 
-    uint32_t* bits = (uint32_t*)(smem + (size_t)wave * lds_stride);   // [5][NW]
-    uint32_t* planes = bits + 5 * NW;                                 // [(6A+4)][NW]
-    int* scar = (int*)(planes + (6 * A + 4) * NW);                    // [64] carrier robot of a slot
+    uint32_t* bits = (uint32_t*)(smem + (size_t)wave * lds_stride);   // [5][NW], critic planes first
+    uint32_t* planes = bits + 5 * NW;                                 // [A][6][NW] actor planes
+    int* scar = (int*)(planes + 6 * A * NW);                          // [64] carrier robot of a slot
     int* invc = scar + 64;                                            // [64] critic row -> slot
-    int* invp = invc + 64;                                            // [64] (agent, slot) -> package
+    uint8_t* o2j = (uint8_t*)(invc + 64);                             // [128] 7-bit order -> slot
+    uint8_t* invp = o2j + 128;                                        // [8][64] (agent, rank) -> slot
 
     // ---- loads: robots, packages (+ tracker data), clock ----
     const bool rl = lane < A, pl = lane < P;
@@ -113,21 +176,23 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
     scar[lane] = 0x7f;
 
     // ---- tracker view of each slot (TrkStale / TrkFresh) ----
+    // ord7: the dict order as 7 bits -- survivors of earlier episodes by their
+    // rank (< P <= 64), then this episode's entries by slot (MDL state words).
     bool pres, trans;
     uint64_t dat;
-    uint32_t ord;
+    uint32_t ord7;
     if (STALE) {
         pres = (f & PS_PRESENT) != 0;
         trans = (f & PS_TRANSIT) != 0;
         const bool sv = (f & PS_SURVIVOR) != 0;
         dat = sv ? tdd : pkd;
-        ord = sv ? f >> PS_RANK_SHIFT : ORD_EPISODE + (uint32_t)lane;
+        ord7 = sv ? (f >> PS_RANK_SHIFT) & 63u : 64u + (uint32_t)lane;
     } else {
         const uint32_t s = f & PS_STATUS;
         pres = s == ST_WAITING || s == ST_IN_TRANSIT;
         trans = s == ST_IN_TRANSIT;
         dat = pkd;
-        ord = (uint32_t)lane;
+        ord7 = (uint32_t)lane;
     }
     pres = pres && pl;
     trans = trans && pres;
@@ -150,7 +215,7 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
     const int ctr_r = cell_r(g_tg), ctr_c = cell_c(g_tg);
     const int cidx = rr * W + rc, tidx = ctr ? ctr_r * W + ctr_c : -1;
 
-    // ---- cell bitsets, carriers ----
+    // ---- cell bitsets, carriers, critic order, order map ----
     wave_sync();
     if (rl) {
         const uint32_t m = 1u << (cidx & 31);
@@ -166,84 +231,55 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
         const int ci = tr * W + tc;
         atomicOr(&bits[BS_ATARGET * NW + (ci >> 5)], 1u << (ci & 31));
     }
-    // critic package rows: active slots in id (= slot) order
     const uint64_t actm = ballot(actv);
     const int cpos = popc64(actm & lanemask_lt());
     const int nact = popc64(actm);
-    if (actv) invc[cpos] = lane;
+    if (actv) invc[cpos] = lane;   // critic package rows: active slots in id (= slot) order
+    if (pres) o2j[ord7] = (uint8_t)lane;
     wave_sync();
 
     // ---- maps ----
     float* am = amap ? amap + (size_t)w * A * 6 * HW : nullptr;
     float* cm = cmap ? cmap + (size_t)w * 4 * HW : nullptr;
-    if (am || cm) {
-        const int npl = (6 * A + 4) * NW;
+    const bool f4 = (HW & 3) == 0;
+    if (am) {
+        // actor planes of agent a at word wd, one lane per (a, wd)
         const float inv_nw = 1.0f / (float)NW;
-        // uniform trip count: the robot gathers below need every lane active
-        for (int k0 = 0; k0 < npl; k0 += WAVE) {
+        for (int k0 = 0; k0 < A * NW; k0 += WAVE) {   // uniform trip count: bperm needs every lane
             const int k = k0 + lane;
-            const int pp = fdivi(k, NW, inv_nw);
-            const int wd = k - pp * NW;
+            const int a = k < A * NW ? fdivi(k, NW, inv_nw) : 0;
+            const int wd = k - a * NW;
             const int base = wd << 5;
-            const uint32_t g = bits[BS_GRID * NW + wd], rb = bits[BS_ROBOT * NW + wd];
-            const uint32_t ws = bits[BS_WSTART * NW + wd], at = bits[BS_ATARGET * NW + wd];
-            const uint32_t mu = bits[BS_MULTI * NW + wd];
-            const int a = pp / 6, ch = pp - 6 * a;   // a >= A: critic plane ch - 6(a - A)
-            const int asrc = a < A ? a : 0;
-            const unsigned od = (unsigned)(bperm(cidx, asrc) - base), td = (unsigned)(bperm(tidx, asrc) - base);
-            const uint32_t ow = od < 32u ? 1u << od : 0u;
-            const uint32_t tw = td < 32u ? 1u << td : 0u;   // no carried target: -1
-            uint32_t v;
-            if (pp < 6 * A) {
-                v = ch == 0 ? g : ch == 1 ? ow : ch == 2 ? ((rb & ~ow) | mu) : ch == 3 ? ws : ch == 4 ? at : tw;
-            } else {
-                const int cc = pp - 6 * A;
-                v = cc == 0 ? g : cc == 1 ? rb : cc == 2 ? ws : at;
+            const unsigned od = (unsigned)(bperm(cidx, a) - base), td = (unsigned)(bperm(tidx, a) - base);
+            if (k < A * NW) {
+                const uint32_t ow = od < 32u ? 1u << od : 0u;
+                const uint32_t tw = td < 32u ? 1u << td : 0u;   // no carried target: -1
+                uint32_t* pa = planes + a * 6 * NW + wd;
+                pa[0] = bits[BS_GRID * NW + wd];
+                pa[NW] = ow;
+                pa[2 * NW] = (bits[BS_ROBOT * NW + wd] & ~ow) | bits[BS_MULTI * NW + wd];
+                pa[3 * NW] = bits[BS_WSTART * NW + wd];
+                pa[4 * NW] = bits[BS_ATARGET * NW + wd];
+                pa[5 * NW] = tw;
             }
-            if (k < npl) planes[k] = v;
         }
         wave_sync();
-        const bool f4 = (HW & 3) == 0;
-        if (am) {
-            if (f4 && ((uintptr_t)am & 15) == 0) emit_planes(planes, NW, 6 * A, HW, am);
-            else emit_planes_dword(planes, NW, 6 * A, HW, am);
-        }
-        if (cm) {
-            if (f4 && ((uintptr_t)cm & 15) == 0) emit_planes(planes + 6 * A * NW, NW, 4, HW, cm);
-            else emit_planes_dword(planes + 6 * A * NW, NW, 4, HW, cm);
-        }
+        if (f4 && ((uintptr_t)am & 15) == 0) emit_planes(planes, NW, 6 * A, HW, am);
+        else emit_planes_dword(planes, NW, 6 * A, HW, am);
+    }
+    if (cm) {   // critic planes = bitsets 0..3 (grid, robots, waiting starts, active targets)
+        if (f4 && ((uintptr_t)cm & 15) == 0) emit_planes(bits, NW, 4, HW, cm);
+        else emit_planes_dword(bits, NW, 4, HW, cm);
     }
 
     // ---- actor vectors (MAPPO/helper.py:68-165) ----
     if (avec) {
         const int Dv = 6 + 5 * MO + 5 * MP + 1;
         float* av = avec + (size_t)w * A * Dv;
-        // tuple lanes: q < A*A other robots (agent q/A, robot q%A); then A*MPc package
-        // slots (agent, slot); then A self tuples
-        const int nq_o = A * A, nq_p = A * MPc;
-        const int q = lane;
-        const bool is_o = q < nq_o, is_p = !is_o && q < nq_o + nq_p, is_s = !is_o && !is_p && q < nq_o + nq_p + A;
-        int qa, qb;   // agent, and other robot / package slot / (self) agent
-        if (is_o) {
-            qa = q / A;
-            qb = q - qa * A;
-        } else if (is_p) {
-            qa = (q - nq_o) / MPc;
-            qb = q - nq_o - qa * MPc;
-        } else {
-            qa = is_s ? q - nq_o - nq_p : 0;
-            qb = qa;
-        }
-        const int ra = bperm(rr, qa), ca = bperm(rc, qa);
-        const int ro = bperm(rr, qb), co = bperm(rc, qb);
-        const bool ovalid = is_o && qb != qa;
-        // other-robot key (rank, index) -- its rank gather issued with the package keys'
-        const int orank = rank[rOff + (ro - ra) * rW + (co - ca)];
-        // waiting-package selection: per agent the MPc smallest (max(0,dl-t), rank, order)
-        // keys by repeated wave minima; (agent a, slot s) -> package lane in invp[a*8+s]
+        // package order of each agent: (max(0,dl-t), distance rank, dict order) ascending
         const int np = popc64(ballot(wt));
         const int want = np < MPc ? np : MPc;
-        const int dsh = p.key32_dsh;
+        const int dsh = p.key7_dsh;
         uint32_t key[8];
 #pragma unroll
         for (int a = 0; a < 8; a++) {
@@ -251,63 +287,96 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
             if (a < A) {
                 const int ra_ = rdl(rr, a), ca_ = rdl(rc, a);
                 const uint32_t rk = rank[rOff + (sr - ra_) * rW + (sc - ca_)];
-                key[a] = wt ? ((uint32_t)dlc << dsh) | (rk << 11) | ord : 0xffffffffu;
+                key[a] = wt ? ((uint32_t)dlc << dsh) | (rk << 7) | ord7 : 0xffffffffu;
             }
         }
-        for (int s = 0; s < want; s++) {
+        if (want <= 6) {
+            // a few slots: repeated wave minima (keys are unique)
+            for (int s = 0; s < want; s++) {
+#pragma unroll
+                for (int a = 0; a < 8; a++) {
+                    if (a < A) {
+                        const uint32_t m = wave_min_u32(key[a]);
+                        const bool hit = key[a] == m;
+                        if (hit) invp[a * 64 + s] = (uint8_t)lane;
+                        key[a] = hit ? 0xffffffffu : key[a];
+                    }
+                }
+            }
+        } else {
 #pragma unroll
             for (int a = 0; a < 8; a++) {
                 if (a < A) {
-                    const uint32_t m = wave_min_u32(key[a]);
-                    const bool hit = key[a] == m;
-                    if (hit) invp[a * 8 + s] = lane;
-                    key[a] = hit ? 0xffffffffu : key[a];
+                    const uint32_t sk = sort64_u32(key[a]);
+                    if (lane < want) invp[a * 64 + lane] = o2j[sk & 127u];
                 }
             }
         }
-        const int okey = ovalid ? (orank << 3) | qb : 0x7fffffff;
-        int opos = 0;
-        for (int k = 0; k < A; k++) opos += bperm(okey, qa * A + k) < okey;
+        // Tuple lanes: q < A*A other robots (agent q/A, robot q%A); then A*MPc package
+        // slots (agent, slot); then A self tuples.  Other robots fit the first pass
+        // (A <= 8), so their positions come from bpermutes within it.
+        const int nq_o = A * A, nq_p = A * MPc, ntup = nq_o + nq_p + A;
+        const float inv_a = 1.0f / (float)A, inv_mpc = MPc > 0 ? 1.0f / (float)MPc : 0.0f;
         wave_sync();
-        const int j = is_p ? invp[qa * 8 + qb] : 0;
-        const bool phas = is_p && qb < want;
-        // the operands: robot qb (self / other) or package j (package slot)
-        const int pj = phas ? j : 0;
-        const int p_sc = bperm(scl, pj), p_tg = bperm(tgl, pj), p_dl = bperm(dlc, pj);
-        const int rsrc = is_o ? qb : qa;   // robot whose carried target is reported
-        const int o_cy = bperm(carry, rsrc), o_ctr = bperm((int)ctr, rsrc);
-        const int o_tr = bperm(ctr_r, rsrc), o_tc = bperm(ctr_c, rsrc), o_dl = bperm(g_dl, rsrc);
-        int x1, x2, x3, x4, x5;
-        if (is_p) {
-            x1 = phas ? cell_r(p_sc) - ra : 0;
-            x2 = phas ? cell_c(p_sc) - ca : 0;
-            x3 = phas ? cell_r(p_tg) - ra : 0;
-            x4 = phas ? cell_c(p_tg) - ca : 0;
-            x5 = phas ? p_dl : 0;
-        } else {
-            const int br = is_o ? ro : ra, bc = is_o ? co : ca;   // the robot described
-            x1 = is_o ? ro - ra : ra;
-            x2 = is_o ? co - ca : ca;
-            const bool ht = o_cy != 0 && o_ctr != 0;
-            x3 = ht ? o_tr - br : 0;
-            x4 = ht ? o_tc - bc : 0;
-            x5 = ht ? o_dl : 0;
-        }
-        const float d1 = qdiv_r(x1, yH), d2 = qdiv_r(x2, yW), d3 = qdiv_r(x3, yH), d4 = qdiv_r(x4, yW);
-        const float d5 = qdiv_r(x5, yT);   // x5 = 0 when T <= 0
-        const float fl = o_cy != 0 ? 1.0f : 0.0f;
-        const bool wr = (is_o && ovalid && opos < MO) || is_p || is_s;
-        if (wr) {
-            const int off = qa * Dv + (is_s ? 0 : is_o ? 6 + 5 * opos : 6 + 5 * MO + 5 * qb);
-            float* o = av + off;
-            o[0] = d1;
-            o[1] = d2;
-            o[2] = is_p ? d3 : fl;
-            o[3] = is_p ? d4 : d3;
-            o[4] = is_p ? d5 : d4;
-            if (is_s) {
-                o[5] = d5;
-                o[Dv - 1] = qdiv_r(t, yT);   // yT = 0 when T <= 0
+        for (int q0 = 0; q0 < ntup; q0 += WAVE) {   // uniform trip count
+            const int q = q0 + lane;
+            const bool is_o = q < nq_o, is_p = !is_o && q < nq_o + nq_p, is_s = !is_o && !is_p && q < ntup;
+            int qa, qb;   // agent, and other robot / package slot / (self) agent
+            if (is_o) {
+                qa = fdivi(q, A, inv_a);
+                qb = q - qa * A;
+            } else if (is_p) {
+                qa = fdivi(q - nq_o, MPc, inv_mpc);
+                qb = q - nq_o - qa * MPc;
+            } else {
+                qa = is_s ? q - nq_o - nq_p : 0;
+                qb = qa;
+            }
+            const int ra = bperm(rr, qa), ca = bperm(rc, qa);
+            const int ob = is_o ? qb : 0;
+            const int ro = bperm(rr, ob), co = bperm(rc, ob);
+            const bool ovalid = is_o && qb != qa;
+            const int orank = rank[rOff + (ro - ra) * rW + (co - ca)];
+            const int okey = ovalid ? (orank << 3) | qb : 0x7fffffff;   // (rank, robot index)
+            int opos = 0;
+            for (int k = 0; k < A; k++) opos += bperm(okey, (qa * A + k) & 63) < okey;
+            const bool phas = is_p && qb < want;
+            const int pj = phas ? invp[qa * 64 + qb] : 0;
+            const int p_sc = bperm(scl, pj), p_tg = bperm(tgl, pj), p_dl = bperm(dlc, pj);
+            const int rsrc = is_o ? qb : qa;   // the robot a self / other tuple describes
+            const int o_cy = bperm(carry, rsrc), o_ctr = bperm((int)ctr, rsrc);
+            const int o_tr = bperm(ctr_r, rsrc), o_tc = bperm(ctr_c, rsrc), o_dl = bperm(g_dl, rsrc);
+            int x1, x2, x3, x4, x5;
+            if (is_p) {
+                x1 = phas ? cell_r(p_sc) - ra : 0;
+                x2 = phas ? cell_c(p_sc) - ca : 0;
+                x3 = phas ? cell_r(p_tg) - ra : 0;
+                x4 = phas ? cell_c(p_tg) - ca : 0;
+                x5 = phas ? p_dl : 0;
+            } else {
+                const int br = is_o ? ro : ra, bc = is_o ? co : ca;
+                x1 = is_o ? ro - ra : ra;
+                x2 = is_o ? co - ca : ca;
+                const bool ht = o_cy != 0 && o_ctr != 0;
+                x3 = ht ? o_tr - br : 0;
+                x4 = ht ? o_tc - bc : 0;
+                x5 = ht ? o_dl : 0;
+            }
+            const float d1 = qdiv_r(x1, yH), d2 = qdiv_r(x2, yW), d3 = qdiv_r(x3, yH), d4 = qdiv_r(x4, yW);
+            const float d5 = qdiv_r(x5, yT);   // x5 = 0 when T <= 0
+            const float fl = o_cy != 0 ? 1.0f : 0.0f;
+            if ((ovalid && opos < MO) || is_p || is_s) {
+                const int off = qa * Dv + (is_s ? 0 : is_o ? 6 + 5 * opos : 6 + 5 * MO + 5 * qb);
+                float* o = av + off;
+                o[0] = d1;
+                o[1] = d2;
+                o[2] = is_p ? d3 : fl;
+                o[3] = is_p ? d4 : d3;
+                o[4] = is_p ? d5 : d4;
+                if (is_s) {
+                    o[5] = d5;
+                    o[Dv - 1] = qdiv_r(t, yT);   // yT = 0 when T <= 0
+                }
             }
         }
         // padding: other-robot slots [MOc, MO) and package slots [MPc, MP) of every agent
@@ -325,12 +394,10 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
         float* cv = cvec + (size_t)w * Dg;
         const int nr = A < MR ? A : MR;
         const int npr = nact < MPsc ? nact : MPsc;
-        // uniform trip count (ds_bpermute reads inactive lanes as 0): stores masked
-        for (int q0 = 0; q0 < nr + npr; q0 += WAVE) {
+        for (int q0 = 0; q0 < nr + npr; q0 += WAVE) {   // uniform trip count: bperm needs every lane
             const int q = q0 + lane;
             const bool isr = q < nr, live = q < nr + npr;
             const int j = (isr || !live) ? 0 : invc[q - nr];
-            // package j's row operands (gathered for every lane; robot lanes use their own)
             const int p_sc = bperm(scl, j), p_tg = bperm(tgl, j), p_dl = bperm(dlc, j);
             const int p_tr = bperm((int)trans, j), p_car = scar[j];
             const int rq = q & 63;

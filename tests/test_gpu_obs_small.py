@@ -40,6 +40,9 @@ CASES = [
     ("map2.txt", 3, 64, 40, "fresh", 2, 8, 100, 30, 0),          # P = 64, obsT = 0
     ("map3.txt", 7, 30, 25, "mappo", 6, 1, 8, 30, 17),           # A = 7 (63 tuple lanes), one package slot, obsT < T
     ("map1.txt", 1, 10, 20, "mappo", 0, 3, 1, 5, None),          # one robot
+    ("map1.txt", 5, 50, 60, "mappo", 100, 100, 100, 100, None),  # config 3b (helper defaults): bitonic order
+    ("map4.txt", 8, 64, 30, "fresh", 7, 64, 8, 64, None),        # A = 8, P = MP = 64: full sort, many tuple passes
+    ("map5.txt", 6, 40, 45, "mappo", 3, 9, 4, 25, 50),           # MO < A-1, 9 slots, obsT > T
 ]
 
 

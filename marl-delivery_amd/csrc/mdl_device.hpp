@@ -169,6 +169,27 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Two independent wave minima with their DPP stages interleaved: each stage of
+// one chain fills the other's DPP read-after-write wait states.
+__device__ __forceinline__ void wave_min_u32x2(uint32_t u, uint32_t v, uint32_t& mu, uint32_t& mv) {
+    const int id = (int)0xffffffff;
+    uint32_t a, b;
+#define MDL_MIN2(ctl, rm)                                                                  \
+    a = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)u, ctl, rm, 0xf, false);            \
+    b = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, ctl, rm, 0xf, false);            \
+    u = a < u ? a : u;                                                                     \
+    v = b < v ? b : v;
+    MDL_MIN2(0x111, 0xf)  // row_shr:1
+    MDL_MIN2(0x112, 0xf)  // row_shr:2
+    MDL_MIN2(0x114, 0xf)  // row_shr:4
+    MDL_MIN2(0x118, 0xf)  // row_shr:8
+    MDL_MIN2(0x142, 0xa)  // row_bcast:15
+    MDL_MIN2(0x143, 0xc)  // row_bcast:31
+#undef MDL_MIN2
+    mu = (uint32_t)__builtin_amdgcn_readlane((int)u, 63);
+    mv = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // float32(a / b) for an int a and an int b > 0 whose fp64 reciprocal y = RN(1/b)
 // is precomputed: RN_f32(RN_f64(a * y)).  Exact (== qdiv) for |a| < 2^24,
 // b < 2^24: a*y is within 2^-52 (relative) of a/b, while a/b is either a float
@@ -196,6 +217,11 @@ __device__ __forceinline__ int cell_r(int pc) { return pc & 255; }
 __device__ __forceinline__ int cell_c(int pc) { return (pc >> 8) & 255; }
 __device__ __forceinline__ int manhattan(int a, int b) {
     return abs(cell_r(a) - cell_r(b)) + abs(cell_c(a) - cell_c(b));
+}
+// The same distance in one v_sad_u8 (sum of |byte differences|): valid for
+// packed cells (bits 16..31 zero), which every cell word of the step kernel is.
+__device__ __forceinline__ int manhattan_sad(int a, int b) {
+    return (int)__builtin_amdgcn_sad_u8((uint32_t)a, (uint32_t)b, 0u);
 }
 
 __device__ __forceinline__ int pk_start(uint64_t v) { return (int)(v & 0xffff); }
@@ -478,7 +504,7 @@ __device__ inline float shaped_agent(const Trk& trk, const float* C, bool active
 }
 
 // np_sum_lanes for n <= 8 (the sequential n < 8 branch, and the 8-partial form at n == 8),
-// with the readlanes issued up front.
+// with the readlanes issued up front.  Lanes n..7 must hold +0.0f.
 __device__ inline float np_sum_lanes8(float v, int n) {
     float x[8];
 #pragma unroll
@@ -487,9 +513,11 @@ __device__ inline float np_sum_lanes8(float v, int n) {
     if (n == 8) {
         res = ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
     } else {
+        // lanes n..6 hold +0.0f, and adding +0.0f is exact here (no partial sum
+        // is ever -0.0f), so the n-term sequential sum needs no selects
         res = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 7; i++) res = i < n ? res + x[i] : res;
+        for (int i = 0; i < 7; i++) res = res + x[i];
     }
     return 0.0f + res;
 }

@@ -567,52 +567,72 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             const bool need_can = (Mact & Mop1 & Mpc0 & Mc0) != 0u;
             bool wv[NCH];
             int stc[NCH];
-            uint64_t anyw = 0;
+            uint32_t klo[NCH];  // low key bits: order key << 10 | slot, or ~0 for no candidate
+            uint64_t wvm[NCH], anyw = 0;
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 const uint32_t f = ps0[c];
                 const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
                 wv[c] = waiting && pk_st(td[c]) <= t0;
                 stc[c] = pk_start(td[c]);
-                anyw |= ballot(wv[c]);
+                klo[c] = wv[c] ? (tq[c] << 10) | (uint32_t)(c * WAVE + lane) : 0xffffffffu;
+                wvm[c] = ballot(wv[c]);
+                anyw |= wvm[c];
             }
             STAMP(7);
             // per-agent answers: bit masks in SGPRs, the nearest start cell written
             // into the agent's lane
-            uint64_t idle_m = 0, can_m = 0;
+            uint32_t Midle = 0, Mcan = 0;
             int best_cell = -1;
             if (anyw && !(MDL_ABLATE & 32)) {
-                for (uint64_t q = ballot(need_near || need_idle); q; q &= q - 1) {
+                // key = distance << 21 | order key << 10 | slot (distance <= 508,
+                // order keys < 0x800, slots < 1024): the minimum names the nearest
+                // package with the reference's tie-break and carries its slot
+                uint64_t q = ballot(need_near || need_idle);
+                if constexpr (NCH == 1) {
+                    // two agents per pass: their minima interleave
+                    for (; q & (q - 1); q &= q - 1, q &= q - 1) {
+                        const int a = ffs64(q), b = ffs64(q & (q - 1));
+                        const int pa = rdl(pcell, a), pb = rdl(pcell, b);
+                        uint32_t ka, kb;
+                        wave_min_u32x2(((uint32_t)manhattan_sad(pa, stc[0]) << 21) | klo[0],
+                                       ((uint32_t)manhattan_sad(pb, stc[0]) << 21) | klo[0], ka, kb);
+                        const int ca = rdl(stc[0], (int)(ka & 63u)), cb = rdl(stc[0], (int)(kb & 63u));
+                        const bool sa = lane == a, sb = lane == b;
+                        Midle = ((sa && (ka >> 21) <= 3u) || (sb && (kb >> 21) <= 3u)) ? ~0u : Midle;
+                        best_cell = sa ? ca : sb ? cb : best_cell;
+                    }
+                }
+                for (; q; q &= q - 1) {
                     const int a = ffs64(q);
                     const int pa = rdl(pcell, a);
-                    uint32_t key[NCH];
                     uint32_t kmin = 0xffffffffu;
 #pragma unroll
                     for (int c = 0; c < NCH; c++) {
-                        key[c] = wv[c] ? ((uint32_t)manhattan(pa, stc[c]) << 11) | tq[c] : 0xffffffffu;
-                        const uint32_t m = wave_min_u32(key[c]);
+                        const uint32_t key = ((uint32_t)manhattan_sad(pa, stc[c]) << 21) | klo[c];
+                        const uint32_t m = wave_min_u32(key);
                         kmin = m < kmin ? m : kmin;
                     }
-                    int bc = -1;
+                    const int js = (int)(kmin & 1023u);
+                    int bc = rdl(stc[0], js & 63);
 #pragma unroll
-                    for (int c = 0; c < NCH; c++) {
-                        const uint64_t b = ballot(key[c] == kmin);
-                        const int v = rdl(stc[c], ffs64(b) & 63);
-                        bc = b ? v : bc;
+                    for (int c = 1; c < NCH; c++) {
+                        const int v = rdl(stc[c], js & 63);
+                        bc = (js >> 6) == c ? v : bc;
                     }
-                    idle_m |= (uint64_t)((kmin >> 11) <= 3u) << a;
-                    best_cell = lane == a ? bc : best_cell;
+                    const bool sel = lane == a;
+                    Midle = (sel && (kmin >> 21) <= 3u) ? ~0u : Midle;
+                    best_cell = sel ? bc : best_cell;
                 }
                 for (uint64_t q = ballot(need_can); q; q &= q - 1) {
                     const int a = ffs64(q);
                     const int ca = rdl(cell, a);
                     uint64_t h = 0;
 #pragma unroll
-                    for (int c = 0; c < NCH; c++) h |= ballot(wv[c] && stc[c] == ca);
-                    can_m |= (uint64_t)(h != 0) << a;
+                    for (int c = 0; c < NCH; c++) h |= ballot(stc[c] == ca) & wvm[c];
+                    Mcan = (lane == a && h != 0) ? ~0u : Mcan;
                 }
             }
-            const uint32_t Midle = vbit(idle_m, lane), Mcan = vbit(can_m, lane);
             STAMP(8);
             // the constants, pinned in SGPRs
             float cs[9];
@@ -637,7 +657,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             // 3. movement
             const float t3v = fmask(~MS & ~Mmov, cs[SH_STUCK]);
             const int tgt = ipick(~Mpc0 & Mpres, ptg, best_cell);
-            const int db = manhattan(pcell, tgt), da = manhattan(cell, tgt);
+            const int db = manhattan_sad(pcell, tgt), da = manhattan_sad(cell, tgt);  // garbage for tgt < 0: masked
             const uint32_t Mt = lmask(tgt >= 0) & Mmov;
             const float t4v = fmask(Mt & lmask(da < db), cs[SH_CLOSER]) + fmask(Mt & lmask(da > db), cs[SH_AWAY]);
             // 4. idle next to an available package

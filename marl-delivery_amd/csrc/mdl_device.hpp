@@ -503,21 +503,23 @@ __device__ inline float shaped_agent(const Trk& trk, const float* C, bool active
     return active ? s : 0.0f;
 }
 
-// np_sum_lanes for n <= 8 (the sequential n < 8 branch, and the 8-partial form at n == 8),
-// with the readlanes issued up front.  Lanes n..7 must hold +0.0f.
+// np_sum_lanes for n <= AU (the sequential n < 8 branch, and the 8-partial form at n == 8),
+// with the readlanes issued up front.  Lanes n..AU-1 must hold +0.0f.
+template <int AU>
 __device__ inline float np_sum_lanes8(float v, int n) {
+    static_assert(AU >= 1 && AU <= 8, "np_sum_lanes8: 1 <= AU <= 8");
     float x[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) x[i] = rdlf(v, i);
+    for (int i = 0; i < 8; i++) x[i] = i < AU ? rdlf(v, i) : 0.0f;
     float res;
-    if (n == 8) {
+    if (AU == 8 && n == 8) {
         res = ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
     } else {
         // lanes n..6 hold +0.0f, and adding +0.0f is exact here (no partial sum
         // is ever -0.0f), so the n-term sequential sum needs no selects
         res = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 7; i++) res = res + x[i];
+        for (int i = 0; i < (AU < 7 ? AU : 7); i++) res = res + x[i];
     }
     return 0.0f + res;
 }
@@ -541,6 +543,13 @@ __device__ inline float np_sum_lanes(float v, int n) {
         for (; i < n; i++) res = res + rdlf(v, i);
     }
     return 0.0f + res;
+}
+
+// the step kernel's sum: unrolled form for AU > 0 robots, the general one otherwise
+template <int AU>
+__device__ inline float np_sum_step(float v, int n) {
+    if constexpr (AU > 0) return np_sum_lanes8<AU>(v, n);
+    else return np_sum_lanes(v, n);
 }
 
 }  // namespace mdl

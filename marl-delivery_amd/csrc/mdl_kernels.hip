@@ -104,7 +104,7 @@ __device__ inline int do_reset(const DevParams& p, int e, const MapDesc& md, Res
 // insert ids spawned at t that are absent (in id order), then carried ->
 // in_transit, in_transit & not carried -> delete.  An inserted entry's order
 // key is implicit (ORD_EPISODE + slot) until the next reset.
-template <int NCH, bool SMALL = false>
+template <int NCH, int AU = 0>
 __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[NCH], bool (&dirty)[NCH],
                                            const uint64_t (&pk)[NCH], int P, int A, int carry, int t) {
     const int lane = lane_id();
@@ -121,13 +121,13 @@ __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[N
     for (int c = 0; c < NCH; c++) {
         const int id = c * WAVE + lane + 1;
         bool carried = false;
-        if constexpr (SMALL) {  // A <= 8: lanes >= A carry 0 and ids start at 1, so no bound is needed
-            uint32_t ci[8], mn = 0xffffffffu;  // min of (carry_i ^ id): zero iff some robot carries id
+        if constexpr (AU > 0) {  // A <= AU: lanes >= A carry 0 and ids start at 1, so no bound is needed
+            uint32_t ci[AU], mn = 0xffffffffu;  // min of (carry_i ^ id): zero iff some robot carries id
 #pragma unroll
-            for (int i = 0; i < 8; i++) ci[i] = (uint32_t)rdl(carry, i);
+            for (int i = 0; i < AU; i++) ci[i] = (uint32_t)rdl(carry, i);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < 8; i++) mn = min(mn, ci[i] ^ (uint32_t)id);
+            for (int i = 0; i < AU; i++) mn = min(mn, ci[i] ^ (uint32_t)id);
             carried = mn == 0u;
         } else {
             for (int i = 0; i < A; i++) carried |= rdl(carry, i) == id;
@@ -282,9 +282,10 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 #else
 #define MDL_STEP_LB (64 * MDL_STEP_WPB)
 #endif
-// SMALL: A <= 8 robots -- the per-robot scans are unrolled over 8 lanes (independent
+// AU > 0: A <= AU robots (AU = 8, or AU = A exactly for the configs' A = 5) -- the
+// per-robot scans are unrolled over AU lanes (independent
 // readlanes, no loop-carried branch), the latency-critical form at the configs' A = 5.
-template <bool STALE, int NCH, bool FUSED, bool SMALL>
+template <bool STALE, int NCH, bool FUSED, int AU>
 __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t* __restrict__ actions, int fmt,
                                               const int* __restrict__ env_ids, int n, int auto_reset,
                                               double* __restrict__ r_out, float* __restrict__ sh_out,
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             // blocked: a lower-index mover proposes the same cell; occ: the robot
             // now standing on the proposed cell (robots stand on distinct cells)
             int blocked = 0, occ = -1;
-            if constexpr (SMALL) {
+            if constexpr (AU > 0) {
                 // Every test is one compare of this lane's proposal against a readlane'd
                 // scalar, folded into vector registers (hit bits / occupant index): the
                 // chain never hands a vector result to the scalar unit, whose forwarding
@@ -430,23 +431,23 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
                 const int propx = act ? prop : -2, cellx = act ? cell : -3;
                 // Three phases kept apart so no instruction waits on the one before it:
                 // all readlanes, all compares, then the selects.
-                int pj[8], cj[8];
+                int pj[AU], cj[AU];
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
+                for (int j = 0; j < AU; j++) {
                     pj[j] = rdl(propx, j);
                     cj[j] = rdl(cellx, j);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                bool hj[8], oj[8];
+                bool hj[AU], oj[AU];
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
+                for (int j = 0; j < AU; j++) {
                     hj[j] = pj[j] == prop;
                     oj[j] = cj[j] == prop;
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 uint32_t hit = 0;
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
+                for (int j = 0; j < AU; j++) {
                     hit |= hj[j] ? (1u << j) : 0u;
                     occ = oj[j] ? j : occ;
                 }
@@ -670,13 +671,13 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             s = s + t5v;
             s_lane = fmask(Mact, s);
         }
-        const float shaped = (float)rr + (SMALL ? np_sum_lanes8(s_lane, A) : np_sum_lanes(s_lane, A));
+        const float shaped = (float)rr + np_sum_step<AU>(s_lane, A);
 
         STAMP(9);
         // ---- tracker update with the new state; a done env that resets here skips
         // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
         const bool do_rst = done && auto_reset;
-        if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH, SMALL>(ps, td, dirty, pk, P, A, carry, t1);
+        if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH, AU>(ps, td, dirty, pk, P, A, carry, t1);
 
         // ---- reset on done (MAPPO/trainer.py:230-235) ----
         int t_out = t1;
@@ -697,7 +698,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
                 pk[c] = j < P ? L.pk[j] : 0;
                 ps[c] = (j < P ? L.pst[j] : 0u) | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
             }
-            if (STALE) tracker_update_regs<NCH, SMALL>(ps, td, dirty, pk, P, A, 0, 0);
+            if (STALE) tracker_update_regs<NCH, AU>(ps, td, dirty, pk, P, A, 0, 0);
             t_out = 0;
             total_out = 0.0;
             any_rst = true;
@@ -1171,11 +1172,14 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
 #else
     const int threads = 256;
 #endif
-    if (p.A <= 8)
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, true>), dim3(blocks_for(n, wpb)), dim3(threads), lds * wpb, s, p,
+    if (NCH <= 2 && p.A == 5)
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 5 : 8)>), dim3(blocks_for(n, wpb)), dim3(threads),
+                           lds * wpb, s, p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+    else if (p.A <= 8)
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 8>), dim3(blocks_for(n, wpb)), dim3(threads), lds * wpb, s, p,
                            actions, fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
     else
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, false>), dim3(blocks_for(n, wpb)), dim3(threads), lds * wpb, s, p,
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 0>), dim3(blocks_for(n, wpb)), dim3(threads), lds * wpb, s, p,
                            actions, fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
 }
 

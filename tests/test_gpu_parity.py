@@ -224,6 +224,15 @@ def test_vs_oracle_map1(tracker):
     _oracle_compare("map1.txt", 64, 5, 50, 60, 1000, 200, tracker)
 
 
+@pytest.mark.parametrize("mapname,A,P,T", [("map1.txt", 1, 20, 40), ("map1.txt", 3, 50, 40), ("map2.txt", 8, 60, 40),
+                                           ("map1.txt", 7, 30, 40), ("map2.txt", 5, 100, 40),
+                                           ("map2.txt", 5, 200, 40), ("map3.txt", 9, 70, 40)])
+def test_vs_oracle_robot_counts(mapname, A, P, T):
+    """Every step-kernel specialisation: A == 5 exactly (P <= 128), A <= 8 with the
+    robot count at run time (incl. numpy's 8-partial sum at A == 8), the general form."""
+    _oracle_compare(mapname, 32, A, P, T, 300 + A, 90, "mappo")
+
+
 def test_vs_oracle_dense_synthetic():
     _oracle_compare("synthetic64.txt", 16, 16, 100, 50, 77, 120, "mappo", check_every=20)
 

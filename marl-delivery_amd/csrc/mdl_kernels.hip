@@ -285,12 +285,28 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 // AU > 0: A <= AU robots (AU = 8, or AU = A exactly for the configs' A = 5) -- the
 // per-robot scans are unrolled over AU lanes (independent
 // readlanes, no loop-carried branch), the latency-critical form at the configs' A = 5.
+// The step kernel's arguments as one struct: its layout is the kernarg segment's,
+// so the write-back can fetch its pointers from the segment in one late batch.
+struct StepArgs {
+    DevParams p;
+    const uint8_t* actions;
+    const int* env_ids;
+    double* r_out;
+    float* sh_out;
+    uint8_t* done_out;
+    int fmt, n, auto_reset, wpb, lds_stride, K;
+};
+typedef __attribute__((address_space(4))) const StepArgs* KargPtr;
+
 template <bool STALE, int NCH, bool FUSED, int AU>
-__global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t* __restrict__ actions, int fmt,
-                                              const int* __restrict__ env_ids, int n, int auto_reset,
-                                              double* __restrict__ r_out, float* __restrict__ sh_out,
-                                              uint8_t* __restrict__ done_out, int wpb, int lds_stride, int K) {
+__global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
     extern __shared__ __align__(16) unsigned char smem[];
+    const DevParams& p = args.p;
+    const uint8_t* __restrict__ actions = args.actions;
+    const int* __restrict__ env_ids = args.env_ids;
+    double* __restrict__ r_out = args.r_out;
+    const int fmt = args.fmt, n = args.n, auto_reset = args.auto_reset, wpb = args.wpb, lds_stride = args.lds_stride,
+              K = args.K;
 #ifdef MDL_STAMPS
     uint64_t stamp_[16];
 #endif
@@ -362,6 +378,13 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
     int t_cur = (int)esv.x;
     double tot_cur = __hiloint2double((int)esv.w, (int)esv.z);
     bool any_rst = false;
+    GLOBAL double* rop;
+    GLOBAL float* shp;
+    GLOBAL uint8_t* dnp;
+    GLOBAL uint32_t* robw;
+    GLOBAL uint16_t* pstw;
+    GLOBAL uint64_t* trkw;
+    GLOBAL u32x4* esw;
     const int KK = FUSED ? K : 1;
     for (int k = 0; k < KK; k++) {
         int mv = MV_S, op = 0;
@@ -416,6 +439,10 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
         const int prop = cell + ((act && ((vmask >> mv) & 1u)) ? ((mv & 1) ? -dm : dm) : 0);
         const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
         const uint64_t movers = ballot(mover);
+        // the proposed cell's move-validity bits, fetched now (every mover) so the load
+        // overlaps the resolution below; consumed only at write-back, for robots that moved
+        uint32_t pvm = vmask;
+        if (mover && !(MDL_ABLATE & 16)) pvm = p.movevalid[mgoff + cell_r(prop) * mW + cell_c(prop)];
         uint64_t moved = 0;
         STAMP(12);
         if (movers) {
@@ -474,7 +501,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
             STAMP(15);
             if ((moved >> lane) & 1ull) {
                 cell = prop;
-                if (!(MDL_ABLATE & 16)) vmask = p.movevalid[mgoff + cell_r(cell) * mW + cell_c(cell)];  // consumed at write-back
+                vmask = pvm;
             }
         }
         const int n_cost = popc64(moved);
@@ -705,35 +732,51 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(DevParams p, const uint8_t
         }
         t_cur = t_out;
         tot_cur = total_out;
+        // The store pointers of the outputs and of the common write-back, fetched here in
+        // one scalar batch (one scalar-cache round trip instead of one per pointer; they
+        // are not held in SGPRs across the step itself).  Rare stores (episode ends,
+        // resets) reload theirs.
+        {
+            // an opaque copy of the segment pointer: the loads below cannot be hoisted
+            // above this point (where their registers would have to live across the step)
+            KargPtr ka = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(ka));
+            rop = (GLOBAL double*)ka->r_out;
+            shp = (GLOBAL float*)ka->sh_out;
+            dnp = (GLOBAL uint8_t*)ka->done_out;
+            robw = (GLOBAL uint32_t*)ka->p.rob;
+            pstw = (GLOBAL uint16_t*)ka->p.pstate;
+            trkw = (GLOBAL uint64_t*)ka->p.trk;
+            esw = (GLOBAL u32x4*)ka->p.es;
+        }
+        pin(rop); pin(shp); pin(dnp); pin(robw); pin(pstw); pin(trkw); pin(esw);
         if (lane == 0) {
             if (done) {
                 p.ep_total[e] = total;
                 p.ep_len[e] = t1;
             }
             const size_t o = (size_t)k * n_ + w;
-            if (r_out) r_out[o] = rr;
-            if (sh_out) sh_out[o] = shaped;
-            if (done_out) done_out[o] = done ? 1 : 0;
+            if (rop) rop[o] = rr;
+            if (shp) shp[o] = shaped;
+            if (dnp) dnp[o] = done ? 1 : 0;
         }
     }  // steps
 
     STAMP(10);
     // ---- write back only what changed ----
-    // (through the kernel arguments again, not the pinned copies above, so no
-    // pointer stays live in SGPRs across the step)
-    if (act) p.rob[(size_t)e * A + lane] = rob_pack(cell, carry, vmask);
+    if (act) robw[(size_t)e * A + lane] = rob_pack(cell, carry, vmask);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
         if (j < P) {
             const size_t g = (size_t)e * P + j;
-            if (ps[c] != ps_in[c]) p.pstate[g] = (uint16_t)ps[c];
+            if (ps[c] != ps_in[c]) pstw[g] = (uint16_t)ps[c];
             if (any_rst) p.pkg[g] = pk[c];
-            if (STALE && dirty[c]) p.trk[g] = td[c];
+            if (STALE && dirty[c]) trkw[g] = td[c];
         }
     }
     if (lane == 0)
-        ((u32x4*)p.es)[e] = u32x4{(uint32_t)t_cur, 0u, (uint32_t)__double2loint(tot_cur), (uint32_t)__double2hiint(tot_cur)};
+        esw[e] = u32x4{(uint32_t)t_cur, 0u, (uint32_t)__double2loint(tot_cur), (uint32_t)__double2hiint(tot_cur)};
     STAMP(11);
 #ifdef MDL_STAMPS
     if (lane == 0)
@@ -1172,15 +1215,29 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
 #else
     const int threads = 256;
 #endif
+#ifdef MDL_EXP_NOLDS  // profiling builds only: no LDS request (valid only while no env resets)
+    lds = 0;
+#endif
+    StepArgs a;
+    a.p = p;
+    a.actions = actions;
+    a.env_ids = ids;
+    a.r_out = r;
+    a.sh_out = sh;
+    a.done_out = done;
+    a.fmt = fmt;
+    a.n = n;
+    a.auto_reset = auto_reset;
+    a.wpb = wpb;
+    a.lds_stride = (int)lds;
+    a.K = K;
+    const dim3 grid(blocks_for(n, wpb)), block(threads);
     if (NCH <= 2 && p.A == 5)
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 5 : 8)>), dim3(blocks_for(n, wpb)), dim3(threads),
-                           lds * wpb, s, p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 5 : 8)>), grid, block, lds * wpb, s, a);
     else if (p.A <= 8)
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 8>), dim3(blocks_for(n, wpb)), dim3(threads), lds * wpb, s, p,
-                           actions, fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 8>), grid, block, lds * wpb, s, a);
     else
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 0>), dim3(blocks_for(n, wpb)), dim3(threads), lds * wpb, s, p,
-                           actions, fmt, ids, n, auto_reset, r, sh, done, wpb, (int)lds, K);
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 0>), grid, block, lds * wpb, s, a);
 }
 
 template <bool ST, bool FUSED>

@@ -501,7 +501,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
             STAMP(15);
             if ((moved >> lane) & 1ull) {
                 cell = prop;
-                vmask = pvm;
+
             }
         }
         const int n_cost = popc64(moved);
@@ -732,6 +732,12 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
         }
         t_cur = t_out;
         tot_cur = total_out;
+        // Settle the move-validity load here, before the first store: vmcnt counts
+        // stores too, so waiting for it after the (lane-0, branchy) output stores
+        // would wait for those stores' round trip.  (A robot that moved and then
+        // reset takes its new cell's bits from the reset above.)
+        vmask = (((moved >> lane) & 1ull) && !do_rst) ? pvm : vmask;
+        asm volatile("" : "+v"(vmask));
         // The store pointers of the outputs and of the common write-back, fetched here in
         // one scalar batch (one scalar-cache round trip instead of one per pointer; they
         // are not held in SGPRs across the step itself).  Rare stores (episode ends,

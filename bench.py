@@ -258,7 +258,7 @@ def main():
             "eager": {"value": total_agent_steps / wall_eager, "ms_per_step": wall_eager / K * 1e3},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mdl::k_step<true, 1, false>", "kernel_us": kdur_us,
+                         "kernel": "mdl::k_step<true, 1, false, 5>", "kernel_us": kdur_us,
                          "kernel_us_isolated_event_pair": kdur_iso_us,
                          "algorithmic_bytes_per_launch": per_launch_bytes},
             "fused_bench_mode": None if wall_f is None else {

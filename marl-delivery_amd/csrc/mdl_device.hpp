@@ -61,6 +61,7 @@ constexpr uint32_t ORD_EPISODE = 0x400u;
 struct DevParams {
     int E, A, P, T;
     double move_cost, delivery_reward, delay_reward;
+    double cost_sum[9];  // cost_sum[k] = ((0.0 + move_cost) + move_cost) ... k times: env.py:252-257's fold
     float shaping[9];
     int stale;
     int obsT, MO, MP, MR, MPs;

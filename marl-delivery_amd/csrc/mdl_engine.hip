@@ -259,6 +259,13 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     p.move_cost = c.move_cost;
     p.delivery_reward = c.delivery_reward;
     p.delay_reward = c.delay_reward;
+    {
+        double acc = 0.0;
+        for (int k = 0; k < 9; k++) {
+            p.cost_sum[k] = acc;
+            acc += c.move_cost;
+        }
+    }
     for (int i = 0; i < 9; i++) p.shaping[i] = (float)c.shaping[i];  // NEP 50: constants rounded to float32
     p.stale = c.tracker_mode == MDL_TRACKER_MAPPO_STALE;
     p.obsT = c.obs_max_time_steps;

@@ -330,6 +330,8 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
     float c_touch = p.shaping[8];
     const uint8_t* c_touch2 = p.movevalid;
     double* c_touch3 = r_out;
+    double c_touch4 = p.cost_sum[0], c_touch5 = p.cost_sum[8];
+    pin(c_touch4); pin(c_touch5);
     pin(A); pin(P); pin(T); pin(env_map); pin(robp); pin(pkgp); pin(pstp); pin(esp); pin(trkp);
     pin(mW); pin(mgoff); pin(actp); pin(idsp); pin(fmt_); pin(n_); pin(wpb_); pin(c_touch); pin(c_touch2);
     pin(c_touch3);
@@ -550,8 +552,13 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
                 ps[c] = (c * WAVE + lane == j) ? ((ps[c] & ~PS_STATUS) | ST_DELIVERED) : ps[c];
         }
         // reward: fp64 fold in the reference's order (move costs, then deliveries)
-        double rr = 0.0;
-        for (int k = 0; k < n_cost; k++) rr += p.move_cost;
+        double rr;
+        if constexpr (AU > 0) {
+            rr = p.cost_sum[n_cost];  // n_cost <= A <= 8: the same fold, tabulated on the host
+        } else {
+            rr = 0.0;
+            for (int k = 0; k < n_cost; k++) rr += p.move_cost;
+        }
         for (uint64_t m = dmask; m; m &= m - 1) {
             const int i = ffs64(m);
             rr += ((omask >> i) & 1ull) ? p.delivery_reward : p.delay_reward;

@@ -39,16 +39,77 @@ __device__ inline void zero_fill(float* dst, int n) {
     if (tail + lane < n) dst[tail + lane] = 0.0f;
 }
 
-// Planes [0, np) of pl (NW words each, HW cells) as floats at dst, one dword
-// per cell (maps with HW % 4 != 0 or an unaligned destination).
-__device__ inline void emit_planes_dword(const uint32_t* pl, int NW, int np, int HW, float* dst) {
-    const int lane = lane_id();
+// Flat bit image of np output planes of HW cells each: bit p*HW + cell of FB is
+// the value of (plane p, cell), so the planes are packed with no per-plane padding
+// and bit i is float i of the [np][H][W] output.  src(p, c0) returns the 32 bits
+// of plane p starting at cell c0 (bits past the plane's end are don't-care).
+template <class F>
+__device__ inline void build_flat(uint32_t* FB, int np, int HW, F src) {
+    const int nfw = (np * HW + 31) >> 5;
     const float inv = 1.0f / (float)HW;
-    for (int i = lane; i < np * HW; i += WAVE) {
-        const int p = fdivi(i, HW, inv);
-        const int cell = i - p * HW;
-        dst[i] = ((pl[p * NW + (cell >> 5)] >> (cell & 31)) & 1u) ? 1.0f : 0.0f;
+    for (int k = lane_id(); k < nfw; k += WAVE) {
+        const int g0 = k << 5;   // < 2^23: fdivi is exact
+        int p = fdivi(g0, HW, inv);
+        int c0 = g0 - p * HW;
+        uint32_t out = 0;
+        int pos = 0;
+        while (pos < 32 && p < np) {
+            const int nb = min(32 - pos, HW - c0);
+            const uint32_t m = nb >= 32 ? ~0u : ((1u << nb) - 1u);
+            out |= (src(p, c0) & m) << pos;
+            pos += nb;
+            p++;
+            c0 = 0;
+        }
+        FB[k] = out;
     }
+}
+
+// The 32 bits of bitset bs (NW words per set, sets back to back) starting at cell c0.
+__device__ __forceinline__ uint32_t bits_at(const uint32_t* bits, int NW, int bs, int c0) {
+    const uint32_t* w = bits + bs * NW + (c0 >> 5);
+    return __builtin_amdgcn_alignbit(w[1], w[0], (uint32_t)(c0 & 31));
+}
+
+__device__ __forceinline__ uint32_t onehot32(int idx, int c0) {
+    const unsigned d = (unsigned)(idx - c0);
+    return d < 32u ? 1u << d : 0u;
+}
+
+// n floats of a flat bit image at dst (16-B aligned): one float4 per lane per pass.
+// Float q*4..q*4+3 are the 4 bits at bit 4q: word q/8 -- with q = lane + 64k the
+// word offset is lane/8 + 8k and the shift (lane%8)*4 is fixed per lane.  The 4
+// bits are spread to bytes by one 24-bit multiply and converted by v_cvt_f32_ubyteN.
+template <int B>
+__device__ __forceinline__ float cvt_ubyte(uint32_t y) {
+    float f;
+    if constexpr (B == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(y));
+    else if constexpr (B == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(f) : "v"(y));
+    else if constexpr (B == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(f) : "v"(y));
+    else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(f) : "v"(y));
+    return f;
+}
+
+__device__ inline void emit_flat4(const uint32_t* FB, int n, float* dst) {
+    const int lane = lane_id();
+    const int nq = n >> 2;
+    const uint32_t sh = (uint32_t)(lane & 7) << 2;
+    const uint32_t* src = FB + (lane >> 3);
+    GLOBAL char* base = (GLOBAL char*)dst;   // wave-uniform base + 32-bit lane offset
+    for (int q = lane; q < nq; q += WAVE, src += 8) {
+        const uint32_t b = __builtin_amdgcn_ubfe(*src, sh, 4u);
+        const uint32_t y = (b * 0x204081u) & 0x01010101u;   // bit i -> byte i (no carries: b < 16)
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        *(GLOBAL f32x4*)(base + ((uint32_t)q << 4)) = f32x4{cvt_ubyte<0>(y), cvt_ubyte<1>(y), cvt_ubyte<2>(y),
+                                                            cvt_ubyte<3>(y)};
+    }
+    const int i = (nq << 2) + lane;   // n % 4 tail
+    if (i < n) dst[i] = ((FB[i >> 5] >> (i & 31)) & 1u) ? 1.0f : 0.0f;
+}
+
+// The same, one dword per lane (an unaligned destination).
+__device__ inline void emit_flat1(const uint32_t* FB, int n, float* dst) {
+    for (int i = lane_id(); i < n; i += WAVE) dst[i] = ((FB[i >> 5] >> (i & 31)) & 1u) ? 1.0f : 0.0f;
 }
 
 // Lane-mask select with the mask in an SGPR pair: bit l set -> b, else a (one VALU op).
@@ -111,12 +172,13 @@ __device__ inline uint32_t sort64_u32(uint32_t x) {
     return x;
 }
 
-// LDS bytes per wave: bitsets (5 NW words), actor planes (6A NW words), carrier
-// table and critic order (64 words each), order -> slot map (128 B), package
-// order of each agent (8 x 64 B).
+// LDS bytes per wave: bitsets (5 NW words + a guard word), the actor planes' flat
+// image (6A NW words), the critic planes' (4 NW words), carrier table and critic
+// order (64 words each), order -> slot map (128 B), package order of each agent
+// (8 x 64 B), each agent's (cell, carried target) index (16 words).
 __host__ __device__ inline size_t obs_small_lds(int A, int HW) {
     const int NW = (HW + 31) / 32;
-    return 4 * (size_t)((6 * A + 5) * NW) + 2 * 256 + 128 + 512;
+    return 4 * (size_t)((6 * A + 9) * NW + 1) + 2 * 256 + 128 + 512 + 64;
 }
 
 // Eligibility (host and device agree): A <= 8 robots, P <= 64 packages, the
@@ -147,12 +209,14 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
     const uint16_t* rank = p.rank + md.rank_off;
     const int rW = 2 * W - 1, rOff = (H - 1) * rW + (W - 1);   // rank[(dr+H-1)*(2W-1) + dc+W-1]
 
-    uint32_t* bits = (uint32_t*)(smem + (size_t)wave * lds_stride);   // [5][NW], critic planes first
-    uint32_t* planes = bits + 5 * NW;                                 // [A][6][NW] actor planes
-    int* scar = (int*)(planes + 6 * A * NW);                          // [64] carrier robot of a slot
+    uint32_t* bits = (uint32_t*)(smem + (size_t)wave * lds_stride);   // [5][NW] + guard, critic planes first
+    uint32_t* planes = bits + 5 * NW + 1;                             // flat image of the 6A actor planes
+    uint32_t* cplanes = planes + 6 * A * NW;                          // flat image of the 4 critic planes
+    int* scar = (int*)(cplanes + 4 * NW);                             // [64] carrier robot of a slot
     int* invc = scar + 64;                                            // [64] critic row -> slot
     uint8_t* o2j = (uint8_t*)(invc + 64);                             // [128] 7-bit order -> slot
     uint8_t* invp = o2j + 128;                                        // [8][64] (agent, rank) -> slot
+    int* aidx = (int*)(invp + 512);                                   // [8][2] agent's cell, carried target
 
     // ---- loads: robots, packages (+ tracker data), clock ----
     const bool rl = lane < A, pl = lane < P;
@@ -166,6 +230,7 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
         if (STALE) tdd = p.trk[g];
     }
     const int t = p.es[e].t;
+    if (lane == 0) bits[5 * NW] = 0;   // guard word read (and masked off) by bits_at
     for (int k = lane; k < NW; k += WAVE) {
         bits[BS_GRID * NW + k] = p.gridbits[md.bits_off + k];
         bits[BS_ROBOT * NW + k] = 0;
@@ -218,6 +283,8 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
     // ---- cell bitsets, carriers, critic order, order map ----
     wave_sync();
     if (rl) {
+        aidx[2 * lane] = cidx;
+        aidx[2 * lane + 1] = tidx;
         const uint32_t m = 1u << (cidx & 31);
         const uint32_t old = atomicOr(&bits[BS_ROBOT * NW + (cidx >> 5)], m);
         if (old & m) atomicOr(&bits[BS_MULTI * NW + (cidx >> 5)], m);   // a second robot on the cell
@@ -241,35 +308,28 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
     // ---- maps ----
     float* am = amap ? amap + (size_t)w * A * 6 * HW : nullptr;
     float* cm = cmap ? cmap + (size_t)w * 4 * HW : nullptr;
-    const bool f4 = (HW & 3) == 0;
     if (am) {
-        // actor planes of agent a at word wd, one lane per (a, wd)
-        const float inv_nw = 1.0f / (float)NW;
-        for (int k0 = 0; k0 < A * NW; k0 += WAVE) {   // uniform trip count: bperm needs every lane
-            const int k = k0 + lane;
-            const int a = k < A * NW ? fdivi(k, NW, inv_nw) : 0;
-            const int wd = k - a * NW;
-            const int base = wd << 5;
-            const unsigned od = (unsigned)(bperm(cidx, a) - base), td = (unsigned)(bperm(tidx, a) - base);
-            if (k < A * NW) {
-                const uint32_t ow = od < 32u ? 1u << od : 0u;
-                const uint32_t tw = td < 32u ? 1u << td : 0u;   // no carried target: -1
-                uint32_t* pa = planes + a * 6 * NW + wd;
-                pa[0] = bits[BS_GRID * NW + wd];
-                pa[NW] = ow;
-                pa[2 * NW] = (bits[BS_ROBOT * NW + wd] & ~ow) | bits[BS_MULTI * NW + wd];
-                pa[3 * NW] = bits[BS_WSTART * NW + wd];
-                pa[4 * NW] = bits[BS_ATARGET * NW + wd];
-                pa[5 * NW] = tw;
-            }
-        }
-        wave_sync();
-        if (f4 && ((uintptr_t)am & 15) == 0) emit_planes(planes, NW, 6 * A, HW, am);
-        else emit_planes_dword(planes, NW, 6 * A, HW, am);
+        // plane p = (agent p/6, channel p%6): grid, self, other robots, waiting starts,
+        // active targets, own carried target (MAPPO/helper.py:6-66)
+        build_flat(planes, 6 * A, HW, [&](int pp, int c0) -> uint32_t {
+            const int a = pp / 6, ch = pp - 6 * a;
+            const int bs = ch == 0 ? BS_GRID : ch == 3 ? BS_WSTART : ch == 4 ? BS_ATARGET : BS_ROBOT;
+            const uint32_t so = onehot32(aidx[2 * a], c0), to = onehot32(aidx[2 * a + 1], c0);
+            uint32_t v = bits_at(bits, NW, bs, c0);
+            v = ch == 2 ? (v & ~so) | bits_at(bits, NW, BS_MULTI, c0) : v;
+            return ch == 1 ? so : ch == 5 ? to : v;
+        });
     }
-    if (cm) {   // critic planes = bitsets 0..3 (grid, robots, waiting starts, active targets)
-        if (f4 && ((uintptr_t)cm & 15) == 0) emit_planes(bits, NW, 4, HW, cm);
-        else emit_planes_dword(bits, NW, 4, HW, cm);
+    if (cm)   // critic planes = bitsets 0..3 (grid, robots, waiting starts, active targets)
+        build_flat(cplanes, 4, HW, [&](int pp, int c0) -> uint32_t { return bits_at(bits, NW, pp, c0); });
+    wave_sync();
+    if (am) {
+        if (((uintptr_t)am & 15) == 0) emit_flat4(planes, 6 * A * HW, am);
+        else emit_flat1(planes, 6 * A * HW, am);
+    }
+    if (cm) {
+        if (((uintptr_t)cm & 15) == 0) emit_flat4(cplanes, 4 * HW, cm);
+        else emit_flat1(cplanes, 4 * HW, cm);
     }
 
     // ---- actor vectors (MAPPO/helper.py:68-165) ----

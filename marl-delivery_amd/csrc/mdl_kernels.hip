@@ -389,8 +389,10 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
     GLOBAL u32x4* esw;
     const int KK = FUSED ? K : 1;
     for (int k = 0; k < KK; k++) {
-        int mv = MV_S, op = 0;
-        if (act) decode_action(araw, fmt_, mv, op);
+        int mv, op;
+        decode_action(araw, fmt_, mv, op);   // every lane (no exec-masked block), then masked
+        mv = act ? mv : MV_S;
+        op = act ? op : 0;
         if (FUSED && k + 1 < KK) araw = act ? (int)actp[((size_t)(k + 1) * n_ + w) * A + lane] : 0;
         const int t0 = t_cur;
         uint32_t ps0[NCH];
@@ -438,13 +440,14 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
         const int pcell = cell, pcarry = carry;
         // bits 1..4 of vmask only: S / other moves never move; L -256, R +256, U -1, D +1
         const int dm = mv <= MV_R ? 256 : 1;
-        const int prop = cell + ((act && ((vmask >> mv) & 1u)) ? ((mv & 1) ? -dm : dm) : 0);
+        const int dlt = ((vmask >> mv) & 1u) ? ((mv & 1) ? -dm : dm) : 0;
+        const int prop = cell + (int)(lmask(act) & (uint32_t)dlt);   // a vector mask: no exec-masked block
         const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
         const uint64_t movers = ballot(mover);
         // the proposed cell's move-validity bits, fetched now (every mover) so the load
         // overlaps the resolution below; consumed only at write-back, for robots that moved
-        uint32_t pvm = vmask;
-        if (mover && !(MDL_ABLATE & 16)) pvm = p.movevalid[mgoff + cell_r(prop) * mW + cell_c(prop)];
+        // (every lane loads: prop is a cell of the map on every lane, 0 on lanes >= A)
+        uint32_t pvm = (MDL_ABLATE & 16) ? vmask : (uint32_t)p.movevalid[mgoff + cell_r(prop) * mW + cell_c(prop)];
         uint64_t moved = 0;
         STAMP(12);
         if (movers) {

@@ -219,3 +219,30 @@ extern "C" int exp_probe(int which, void* out, int n, int reps, hipStream_t s) {
     }
     return (int)hipGetLastError();
 }
+
+// kernel-argument lines on an exposed chain: NL lines, then one load round trip,
+// then 1024 dependent VALU ops (so the wave outlives the launch floor)
+template <int NL>
+__global__ __launch_bounds__(256) void k_klines_chain(KLines k, const uint32_t* __restrict__ rob,
+                                                      uint32_t* __restrict__ out, int n) {
+    const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+        uint64_t v = k.line[i][i % 8];
+        asm volatile("" : "+s"(v));
+        acc += v;
+    }
+    if (w >= n) return;
+    uint32_t r = lane < 5 ? rob[(size_t)w * 5 + lane] : 0u;
+    r += (uint32_t)acc;
+    asm volatile(".rept 1024\n v_add_u32 %0, %0, %0\n .endr" : "+v"(r));
+    if (lane < 5) out[(size_t)w * 5 + lane] = r;
+}
+extern "C" int exp_klines_chain(int nl, const void* rob, void* out, int n, hipStream_t s) {
+    KLines k{};
+    if (nl == 1) hipLaunchKernelGGL(k_klines_chain<1>, dim3((n + 3) / 4), dim3(256), 0, s, k, (const uint32_t*)rob, (uint32_t*)out, n);
+    else hipLaunchKernelGGL(k_klines_chain<9>, dim3((n + 3) / 4), dim3(256), 0, s, k, (const uint32_t*)rob, (uint32_t*)out, n);
+    return (int)hipGetLastError();
+}

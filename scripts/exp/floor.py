@@ -29,6 +29,8 @@ for E in (1024, 4096):
         "klines3": lambda: L.exp_klines(3, C.c_void_p(rob.data_ptr()), C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
         "klines6": lambda: L.exp_klines(6, C.c_void_p(rob.data_ptr()), C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
         "klines9": lambda: L.exp_klines(9, C.c_void_p(rob.data_ptr()), C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
+        "klchain1": lambda: L.exp_klines_chain(1, C.c_void_p(rob.data_ptr()), C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
+        "klchain9": lambda: L.exp_klines_chain(9, C.c_void_p(rob.data_ptr()), C.c_void_p(ro.data_ptr()), E, C.c_void_p(s.cuda_stream)),
         "rt2": lambda: L.exp_rt2(C.c_void_p(rob.data_ptr()), C.c_void_p(pkg.data_ptr()), C.c_void_p(tab.data_ptr()), C.c_void_p(ro.data_ptr()), E, A, P, C.c_void_p(s.cuda_stream)),
     }
     for name, fn in calls.items():

@@ -549,7 +549,7 @@ __device__ inline float np_sum_lanes(float v, int n) {
 // the step kernel's sum: unrolled form for AU > 0 robots, the general one otherwise
 template <int AU>
 __device__ inline float np_sum_step(float v, int n) {
-    if constexpr (AU > 0) return np_sum_lanes8<AU>(v, n);
+    if constexpr (AU > 0 && AU <= 8) return np_sum_lanes8<AU>(v, n);
     else return np_sum_lanes(v, n);
 }
 

@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 #else
 #define MDL_STEP_LB (64 * MDL_STEP_WPB)
 #endif
-// AU > 0: A <= AU robots (AU = 8, or AU = A exactly for the configs' A = 5) -- the
+// AU > 0: A <= AU robots (AU = 8, or AU = A exactly for the configs' A = 5 and 16) -- the
 // per-robot scans are unrolled over AU lanes (independent
 // readlanes, no loop-carried branch), the latency-critical form at the configs' A = 5.
 // The step kernel's arguments as one struct: its layout is the kernarg segment's,
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
                     occ = oj[j] ? j : occ;
                 }
                 // a lower-index mover into the same cell (only lanes < A are movers)
-                blocked = (hit & ((1u << (lane & 7)) - 1u) & (uint32_t)movers) != 0u;
+                blocked = (hit & ((1u << (lane & 31)) - 1u) & (uint32_t)movers) != 0u;
             } else {
                 for (uint64_t m = movers; m; m &= m - 1) {
                     const int j = ffs64(m);
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
         }
         // reward: fp64 fold in the reference's order (move costs, then deliveries)
         double rr;
-        if constexpr (AU > 0) {
+        if constexpr (AU > 0 && AU <= 8) {
             rr = p.cost_sum[n_cost];  // n_cost <= A <= 8: the same fold, tabulated on the host
         } else {
             rr = 0.0;
@@ -1250,6 +1250,8 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
     const dim3 grid(blocks_for(n, wpb)), block(threads);
     if (NCH <= 2 && p.A == 5)
         hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 5 : 8)>), grid, block, lds * wpb, s, a);
+    else if (NCH <= 2 && p.A == 16)   // config 5's robot count
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 16 : 8)>), grid, block, lds * wpb, s, a);
     else if (p.A <= 8)
         hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 8>), grid, block, lds * wpb, s, a);
     else

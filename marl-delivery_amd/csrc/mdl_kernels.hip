@@ -331,10 +331,14 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
     const uint8_t* c_touch2 = p.movevalid;
     double* c_touch3 = r_out;
     double c_touch4 = p.cost_sum[0], c_touch5 = p.cost_sum[8];
-    pin(c_touch4); pin(c_touch5);
-    pin(A); pin(P); pin(T); pin(env_map); pin(robp); pin(pkgp); pin(pstp); pin(esp); pin(trkp);
-    pin(mW); pin(mgoff); pin(actp); pin(idsp); pin(fmt_); pin(n_); pin(wpb_); pin(c_touch); pin(c_touch2);
-    pin(c_touch3);
+    int c_touch6 = lds_stride;
+    // ONE asm statement pins them all: every load is issued before a single wait
+    // (separate pins let the compiler wait after the first few and issue the rest
+    // -- other kernarg lines, i.e. a second scalar-cache miss -- behind that wait)
+    asm volatile(""
+                 : "+s"(A), "+s"(P), "+s"(T), "+s"(env_map), "+s"(robp), "+s"(pkgp), "+s"(pstp), "+s"(esp),
+                   "+s"(trkp), "+s"(mW), "+s"(mgoff), "+s"(actp), "+s"(idsp), "+s"(fmt_), "+s"(n_), "+s"(wpb_),
+                   "+s"(c_touch), "+s"(c_touch2), "+s"(c_touch3), "+s"(c_touch4), "+s"(c_touch5), "+s"(c_touch6));
     STAMP(1);
 
     const int wave = wave_id();

@@ -10,8 +10,9 @@ import marl_gpu  # noqa: E402
 from marl_gpu.maps import grid_array, load_map, map_path  # noqa: E402
 
 E, A, P, T = 16384, 5, 50, 500
+MO, MP = (int(x) for x in os.environ.get("OBS_MO_MP", "4,5").split(","))   # config 3b: 100,100
 env = marl_gpu.BatchedEnv(grid_array(load_map(map_path("map1.txt"))), E, A, P, T, seed=42, tracker="mappo",
-                          max_other_robots=4, max_packages_obs=5)
+                          max_other_robots=MO, max_packages_obs=MP)
 env.reset()
 g = torch.Generator(device="cuda").manual_seed(0)
 for k in range(60):

@@ -372,12 +372,14 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
                 }
             }
         }
-        // Tuple lanes: q < A*A other robots (agent q/A, robot q%A); then A*want package
-        // slots (agent, slot) -- only the filled ones: slots [want, MP) are zero-filled
-        // with float4 stores below; then A self tuples.  Other robots fit the first pass
+        // Tuple lanes: q < A*A other robots (agent q/A, robot q%A); then A*ns package
+        // slots (agent, slot); then A self tuples.  ns = MPc when every tuple fits one
+        // pass (empty slots are zero tuples), else ns = want: only the filled slots, the
+        // rest zero-filled with float4 stores below.  Other robots fit the first pass
         // (A <= 8), so their positions come from bpermutes within it.
-        const int nq_o = A * A, nq_p = A * want, ntup = nq_o + nq_p + A;
-        const float inv_a = 1.0f / (float)A, inv_w = want > 0 ? 1.0f / (float)want : 0.0f;
+        const int nq_o = A * A, ns = nq_o + A * MPc + A <= WAVE ? MPc : want;
+        const int nq_p = A * ns, ntup = nq_o + nq_p + A;
+        const float inv_a = 1.0f / (float)A, inv_w = ns > 0 ? 1.0f / (float)ns : 0.0f;
         wave_sync();
         for (int q0 = 0; q0 < ntup; q0 += WAVE) {   // uniform trip count
             const int q = q0 + lane;
@@ -387,8 +389,8 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
                 qa = fdivi(q, A, inv_a);
                 qb = q - qa * A;
             } else if (is_p) {
-                qa = fdivi(q - nq_o, want, inv_w);
-                qb = q - nq_o - qa * want;
+                qa = fdivi(q - nq_o, ns, inv_w);
+                qb = q - nq_o - qa * ns;
             } else {
                 qa = is_s ? q - nq_o - nq_p : 0;
                 qb = qa;
@@ -440,11 +442,11 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
                 }
             }
         }
-        // padding: other-robot slots [MOc, MO) and package slots [want, MP) of every agent
-        if (MO > MOc || MP > want) {
+        // padding: other-robot slots [MOc, MO) and package slots [ns, MP) of every agent
+        if (MO > MOc || MP > ns) {
             for (int a = 0; a < A; a++) {
                 zero_fill(av + a * Dv + 6 + 5 * MOc, 5 * (MO - MOc));
-                zero_fill(av + a * Dv + 6 + 5 * MO + 5 * want, 5 * (MP - want));
+                zero_fill(av + a * Dv + 6 + 5 * MO + 5 * ns, 5 * (MP - ns));
             }
         }
     }

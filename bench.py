@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--fused-k", type=int, default=100, help="bench mode (ii): steps per fused launch (0 = skip)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches only (PMC profiling passes)")
+    ap.add_argument("--graph-only", action="store_true",
+                    help="skip the eager and isolated-launch legs (rocprof kernel-trace pass: the trace then holds "
+                         "only the warmup and the timed graph replay, so its average is the timed region's)")
     return ap.parse_args()
 
 
@@ -173,12 +176,14 @@ def main():
     gpu_ms = ev0.elapsed_time(ev1)
 
     # ---- eager throughput (same kernels, one ctypes launch per step) ----
-    barrier()
-    t1 = time.perf_counter()
-    for k in range(K):
-        one(k)
-    barrier()
-    wall_eager = time.perf_counter() - t1
+    wall_eager = None
+    if not args.graph_only:
+        barrier()
+        t1 = time.perf_counter()
+        for k in range(K):
+            one(k)
+        barrier()
+        wall_eager = time.perf_counter() - t1
 
     # ---- bench mode: fused_k steps per launch, each env's
     # state in registers between steps; same action stream; not the API path ----
@@ -202,20 +207,23 @@ def main():
     # gap between kernels and is an upper bound on the rocprof kernel time);
     # plus an isolated per-launch event pair for reference ----
     kdur_us = gpu_ms / K * 1e3
-    nk = min(K, 200)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
-    for k in range(nk):
-        starts[k].record()
-        one(k)
-        ends[k].record()
-    torch.cuda.synchronize()
-    kdur_iso_us = float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]) * 1e3)
+    kdur_iso_us = None
+    if not args.graph_only:
+        nk = min(K, 200)
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
+        for k in range(nk):
+            starts[k].record()
+            one(k)
+            ends[k].record()
+        torch.cuda.synchronize()
+        kdur_iso_us = float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]) * 1e3)
 
     if dist is not None:
-        t = torch.tensor([wall, wall_eager, wall_f or 0.0], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall, wall_eager or 0.0, wall_f or 0.0], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, wall_eager = float(t[0]), float(t[1])
+        wall = float(t[0])
+        wall_eager = float(t[1]) if wall_eager is not None else None
         wall_f = float(t[2]) if wall_f is not None else None
 
     total_agent_steps = E * A * K * world
@@ -255,7 +263,8 @@ def main():
                        "envs_per_gpu": E, "agents": A, "packages": P, "max_time_steps": args.T,
                        "parallelism": f"env-shard x{world}"},
             "gpu_event_ms_per_step": gpu_ms / K,
-            "eager": {"value": total_agent_steps / wall_eager, "ms_per_step": wall_eager / K * 1e3},
+            "eager": None if wall_eager is None else {"value": total_agent_steps / wall_eager,
+                                                       "ms_per_step": wall_eager / K * 1e3},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "mdl::k_step<true, 1, false, 5>", "kernel_us": kdur_us,

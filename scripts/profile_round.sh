@@ -10,7 +10,9 @@ TAG=${TAG:-round}
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 B="$R/bench.py --cpu-seconds 0"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $B --steps 2000 --warmup 100 > $O/trace_bench.log 2>&1 || exit $?
+# --graph-only: the trace holds the warmup and the timed graph replay only, so the
+# stats average is the timed region's (bench.py's kernel_us)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $B --graph-only --fused-k 0 --steps 2000 --warmup 20 > $O/trace_bench.log 2>&1 || exit $?
 P="$B --no-graph --fused-k 0 --steps 300 --warmup 20"
 timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex k_step -d $O/sq -o run --output-format csv -- python3 $P > $O/sq.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_step -d $O/fetch -o run --output-format csv -- python3 $P > $O/fetch.log 2>&1 || exit $?

@@ -21,6 +21,7 @@ seg = {"warmup_eager": (0, W), "graph_replay": (W + 1, W + 1 + K), "eager": (W +
        "isolated": (W + 1 + 2 * K, len(d))}
 out = {"kernel": rows[0]["Kernel_Name"], "dispatches": len(d)}
 for k, (a, b) in seg.items():
+    b = min(b, len(d))
     if b > a:
         out[k] = {"n": int(b - a), "mean_ns": float(d[a:b].mean()), "median_ns": float(np.median(d[a:b])),
                   "mean_start_to_start_ns": float(np.mean(np.diff(s[a:b]))) if b - a > 1 else None}

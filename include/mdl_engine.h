@@ -148,6 +148,16 @@ int mdl_load_state(MdlEngine* eng, const void* host_buf, int64_t bytes, void* st
 int mdl_sample_actions(const float* logits, int64_t n_rows, int32_t n_actions, uint64_t seed, uint64_t offset,
                        uint8_t* actions, float* log_probs, void* stream);
 
+/* The same draw with the offset read on the device: offset = *offset_dev + offset_add, so a
+ * captured hipGraph of a whole rollout replays with fresh offsets (MAPPO/trainer.py:141-143:
+ * each rollout samples new actions).  Identical results to mdl_sample_actions at that offset. */
+int mdl_sample_actions_dev(const float* logits, int64_t n_rows, int32_t n_actions, uint64_t seed,
+                           const uint64_t* offset_dev, uint64_t offset_add, uint8_t* actions, float* log_probs,
+                           void* stream);
+
+/* *counter += value on the device (stream-ordered; advances offset_dev inside a graph). */
+int mdl_counter_add(uint64_t* counter, uint64_t value, void* stream);
+
 /* Generalised advantage estimation exactly as MAPPO/trainer.py:266-276 computes it in float32
  * (same operation order): rewards, values, dones [T][n] (dones uint8), next_value [n];
  * gamma = float32(GAMMA), gamma_lambda = float32(GAMMA * GAE_LAMBDA) with the product in double.

@@ -38,11 +38,18 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
 // 24-bit uniform in [0, 1); action = first i with u*S < e_0+..+e_i where
 // e_i = exp(l_i - max) and S = sum e_i (sequential fp32 sums); log_prob =
 // (l_a - max) - log(S).  Rows whose logits are all -inf get action 0, -inf.
+// off_dev (graph-capturable form): the offset is *off_dev + off_lo|off_hi<<32.
 __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ logits, int64_t n_rows, int n_act,
                                                 uint32_t k0, uint32_t k1, uint32_t off_lo, uint32_t off_hi,
-                                                uint8_t* __restrict__ actions, float* __restrict__ log_probs) {
+                                                const uint64_t* __restrict__ off_dev, uint8_t* __restrict__ actions,
+                                                float* __restrict__ log_probs) {
     const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= n_rows) return;
+    if (off_dev) {
+        const uint64_t o = *off_dev + ((uint64_t)off_hi << 32 | off_lo);
+        off_lo = (uint32_t)o;
+        off_hi = (uint32_t)(o >> 32);
+    }
     const float* l = logits + row * n_act;
     float m = -INFINITY;
     for (int i = 0; i < n_act; i++) m = fmaxf(m, l[i]);
@@ -105,6 +112,10 @@ __global__ __launch_bounds__(256) void k_gae(const float* __restrict__ r, const 
     }
 }
 
+__global__ void k_counter_add(uint64_t* __restrict__ c, uint64_t v) {
+    if (threadIdx.x == 0) *c += v;
+}
+
 }  // namespace mdl
 
 namespace {
@@ -127,9 +138,30 @@ int mdl_sample_actions(const float* logits, int64_t n_rows, int32_t n_actions, u
     const int64_t blocks = (n_rows + 255) / 256;
     hipLaunchKernelGGL(mdl::k_sample, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, logits, n_rows,
                        (int)n_actions, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)offset,
-                       (uint32_t)(offset >> 32), actions, log_probs);
+                       (uint32_t)(offset >> 32), (const uint64_t*)nullptr, actions, log_probs);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : rfail("mdl_sample_actions: launch failed", e);
+}
+
+int mdl_sample_actions_dev(const float* logits, int64_t n_rows, int32_t n_actions, uint64_t seed,
+                           const uint64_t* offset_dev, uint64_t offset_add, uint8_t* actions, float* log_probs,
+                           void* stream) {
+    if (!logits || !actions || !offset_dev) return rfail("mdl_sample_actions_dev: null argument");
+    if (n_rows < 0 || n_actions < 1 || n_actions > 256) return rfail("mdl_sample_actions_dev: bad sizes");
+    if (n_rows == 0) return 0;
+    const int64_t blocks = (n_rows + 255) / 256;
+    hipLaunchKernelGGL(mdl::k_sample, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, logits, n_rows,
+                       (int)n_actions, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)offset_add,
+                       (uint32_t)(offset_add >> 32), offset_dev, actions, log_probs);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : rfail("mdl_sample_actions_dev: launch failed", e);
+}
+
+int mdl_counter_add(uint64_t* counter, uint64_t value, void* stream) {
+    if (!counter) return rfail("mdl_counter_add: null argument");
+    hipLaunchKernelGGL(mdl::k_counter_add, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, value);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : rfail("mdl_counter_add: launch failed", e);
 }
 
 int mdl_gae(const float* rewards, const float* values, const float* next_value, const uint8_t* dones, int32_t T,

@@ -65,6 +65,8 @@ SIGNATURES = {
     "mdl_save_state": (C.c_int, [_vp, _vp, C.c_int64, _vp]),
     "mdl_load_state": (C.c_int, [_vp, _vp, C.c_int64, _vp]),
     "mdl_sample_actions": (C.c_int, [_vp, C.c_int64, _i32, C.c_uint64, C.c_uint64, _vp, _vp, _vp]),
+    "mdl_sample_actions_dev": (C.c_int, [_vp, C.c_int64, _i32, C.c_uint64, _vp, C.c_uint64, _vp, _vp, _vp]),
+    "mdl_counter_add": (C.c_int, [_vp, C.c_uint64, _vp]),
     "mdl_gae": (C.c_int, [_vp, _vp, _vp, _vp, _i32, C.c_int64, C.c_float, C.c_float, _vp, _vp, _vp]),
     "mdl_read_state": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mdl_views_features": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32,

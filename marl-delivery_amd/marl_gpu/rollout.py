@@ -37,6 +37,19 @@ def sample_actions(logits: torch.Tensor, seed: int, offset: int, out=None):
     return acts, lp
 
 
+def sample_actions_dev(logits: torch.Tensor, seed: int, offset_dev: torch.Tensor, offset_add: int, out):
+    """``sample_actions`` at offset ``offset_dev[0] + offset_add`` with the base read on the
+    device (uint64 tensor [1]), so the launch can live in a replayed hipGraph."""
+    if logits.dtype != torch.float32 or not logits.is_contiguous():
+        logits = logits.float().contiguous()
+    N, n_act = logits.shape
+    acts, lp = out
+    check(lib().mdl_sample_actions_dev(ptr(logits), N, n_act, seed & (2**64 - 1), ptr(offset_dev),
+                                       offset_add & (2**64 - 1), ptr(acts), ptr(lp), stream_handle(logits.device)),
+          "mdl_sample_actions_dev")
+    return acts, lp
+
+
 def gae(rewards, values, next_value, dones, gamma=0.99, gae_lambda=0.95, out=None):
     """Advantages and returns exactly as MAPPO/trainer.py:266-276 computes them.
 
@@ -93,26 +106,69 @@ class MappoRollout:
         self.mb_values = torch.zeros((T, E), **f)
         self.next_obs = env.obs_buffers(E, H, W)
         self._r_env = torch.zeros(E, dtype=torch.float64, device=dev)
+        self._graph = None          # hipGraph of one whole rollout (collect(graph=True))
+        self._graph_key = None
+        self._graph_out = None
+        self._off_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # sampler offset base (uint64 bits)
 
     def _slot(self, k):
         return dict(actor_map=self.mb_obs[k], actor_vec=self.mb_vector_obs[k], critic_map=self.mb_global_states[k],
                     critic_vec=self.mb_global_vector[k])
 
     @torch.no_grad()
-    def collect(self, actor, critic):
+    def collect(self, actor, critic, graph: bool = False):
+        """One rollout of ``rollout_steps`` env steps.  graph=True: the first call runs
+        eagerly and captures the whole rollout (policy forwards, sampling, steps,
+        observations, GAE) as one hipGraph; later calls with the same actor/critic replay
+        it -- bit-identical to eager calls (the sampler's offset base lives on the
+        device and advances inside the graph).  The returned tensors are the graph's
+        static buffers: consume them before the next collect."""
+        if not graph:
+            return self._run(actor, critic, False)
+        key = (id(actor), id(critic))
+        if self._graph is not None and self._graph_key == key:
+            self._graph.replay()
+            self.offset += self.T
+            return self._graph_out
+        out = self._run(actor, critic, False)        # this call's rollout, and the warm-up
+        self._capture(actor, critic, key)
+        return out
+
+    def _capture(self, actor, critic, key):
+        dev = self.env.device
+        torch.cuda.synchronize(dev)
+        self._off_dev.fill_(self.offset)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        off0 = self.offset
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self._graph_out = self._run(actor, critic, True)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        self.offset = off0   # capture ran nothing
+        self._graph, self._graph_key = g, key
+
+    def _run(self, actor, critic, dev_offset: bool):
         env, T = self.env, self.T
         E, A = env.E, env.A
         env.build_obs(out=self._slot(0))              # current obs = f(current state, tracker)
         for step in range(T):
             obs = self.mb_obs[step]
             logits = actor(obs.reshape(E * A, *obs.shape[2:]), self.mb_vector_obs[step].reshape(E * A, -1))
-            sample_actions(logits, self.seed, self.offset,
-                           out=(self.mb_actions[step].view(-1), self.mb_log_probs[step].view(-1)))
+            acts_lp = (self.mb_actions[step].view(-1), self.mb_log_probs[step].view(-1))
+            if dev_offset:
+                sample_actions_dev(logits, self.seed, self._off_dev, step, out=acts_lp)
+            else:
+                sample_actions(logits, self.seed, self.offset, out=acts_lp)
             self.offset += 1
             self.mb_values[step] = critic(self.mb_global_states[step], self.mb_global_vector[step]).reshape(E)
             env.step(self.mb_actions[step], auto_reset=True,
                      out=(self._r_env, self.mb_rewards[step], self.mb_dones[step]))
             env.build_obs(out=self._slot(step + 1) if step + 1 < T else self.next_obs)
+        if dev_offset:
+            check(lib().mdl_counter_add(ptr(self._off_dev), T, stream_handle(env.device)), "mdl_counter_add")
         next_value = critic(self.next_obs["critic_map"], self.next_obs["critic_vec"]).reshape(E)
         adv, ret = gae(self.mb_rewards, self.mb_values, next_value, self.mb_dones, self.gamma, self.gae_lambda)
         H, W = obs.shape[-2:]

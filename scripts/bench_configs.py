@@ -94,7 +94,7 @@ def run(cfg, steps, warmup):
     env.close()
 
 
-def run_rollout(steps):
+def run_rollout(steps, graph=False):
     """MAPPO rollout on the device: 4096 envs, map1, A=5, the
     trainer's featurizer sizes, a linear actor on the 52-dim vector and a linear
     critic on the 1301-dim vector; sampling, step, obs into the buffers and GAE
@@ -113,15 +113,15 @@ def run_rollout(steps):
     critic = lambda gmap, gvec: gvec @ wc  # noqa: E731
     Tr = 128
     ro = R.MappoRollout(env, Tr, seed=1)
-    ro.collect(actor, critic)
+    ro.collect(actor, critic, graph=graph)   # (graph: this call runs eagerly and captures)
     torch.cuda.synchronize()
     n = max(1, steps // Tr)
     t0 = time.perf_counter()
     for _ in range(n):
-        ro.collect(actor, critic)
+        ro.collect(actor, critic, graph=graph)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    out = {"config": "rollout", "envs": E, "agents": A, "rollout_steps": Tr, "rollouts": n,
+    out = {"config": "rollout_graph" if graph else "rollout", "envs": E, "agents": A, "rollout_steps": Tr, "rollouts": n,
            "us_per_env_step": dt / (n * Tr) * 1e6, "agent_steps_per_s": E * A * n * Tr / dt,
            "note": "MappoRollout.collect: linear actor/critic (torch), on-device sampling, mdl_step, mdl_build_obs "
                    "into the rollout buffers, GAE kernel"}
@@ -136,8 +136,8 @@ def main():
     a = ap.parse_args()
     torch.cuda.set_device(0)
     for c in a.config.split(","):
-        if c == "rollout":
-            run_rollout(a.steps)
+        if c in ("rollout", "rollout_graph"):
+            run_rollout(a.steps, graph=c == "rollout_graph")
         else:
             run(c, a.steps, a.warmup)
 

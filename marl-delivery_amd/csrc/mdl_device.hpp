@@ -348,14 +348,19 @@ __device__ inline int reset_env(MTState& mt, const DevParams& p, const MapDesc& 
     const int N = md.H;
     const int lim = A < 20 ? A : 20;
     for (int i = 0; i < P; i++) {
-        const int start = fl[randint(mt, 0, F)];
-        int target;
+        const int s_idx = randint(mt, 0, F);
+        int t_idx;
         do {
-            target = fl[randint(mt, 0, F)];
-        } while (target == start);
+            t_idx = randint(mt, 0, F);
+        } while (t_idx == s_idx);
         const int to_dl = 10 + randint(mt, N / 2, 3 * N);
         const int st = (i <= lim) ? 0 : randint(mt, 1, p.T);
-        if (lane == 0) scratch[i] = pk_make(start, target, st, st + to_dl);
+        if (lane == 0) scratch[i] = pk_make(s_idx, t_idx, st, st + to_dl);
+    }
+    wave_sync();
+    for (int j = lane; j < P; j += WAVE) {
+        const uint64_t v = scratch[j];
+        scratch[j] = pk_make(fl[pk_start(v)], fl[pk_target(v)], pk_st(v), pk_dl(v));
     }
     wave_sync();
     // stable sort by start_time (env.py:119): rank = #(st_i < st_j) + #(i < j, st_i == st_j)

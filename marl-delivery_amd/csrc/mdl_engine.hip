@@ -143,7 +143,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     if (!cfg || !grids || !map_hw || !out) return fail("mdl_create: null argument");
     *out = nullptr;
     const MdlConfig& c = *cfg;
-    if (c.n_envs < 1) return fail("n_envs must be >= 1");
+    if (c.n_envs < 1 || c.n_envs >= (1 << 24)) return fail("n_envs must be in [1, 2^24)");
     if (c.n_robots < 1 || c.n_robots > MDL_MAX_ROBOTS) return fail("n_robots must be in [1, %d]", MDL_MAX_ROBOTS);
     if (c.n_packages < 1 || c.n_packages > MDL_MAX_PACKAGES)
         return fail("n_packages must be in [1, %d]", MDL_MAX_PACKAGES);

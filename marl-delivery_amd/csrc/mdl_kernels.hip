@@ -298,60 +298,56 @@ struct StepArgs {
 };
 typedef __attribute__((address_space(4))) const StepArgs* KargPtr;
 
+// The step kernel's leading arguments are preloaded into SGPRs by the command
+// processor (gfx950 kernarg preloading, -amdgpu-kernarg-preload-count=14 for this
+// file: 14 dwords): the state pointers, A | P << 16 and n | wpb << 24 | flags.  So
+// the state loads issue at wave start, overlapping the kernel-argument fetch
+// instead of waiting for it.  StepKarg mirrors the kernarg layout.
+struct StepKarg {
+    const uint32_t* rob;
+    const uint64_t* pkg;
+    const uint16_t* pst;
+    const u32x4* es;
+    const uint64_t* trk;
+    const uint8_t* act;
+    uint32_t ap, nw;
+    StepArgs args;
+};
+constexpr uint32_t NW_IDS = 1u << 29, NW_MAP = 1u << 30;
+
 template <bool STALE, int NCH, bool FUSED, int AU>
-__global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
+__global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict__ rob_pre,
+                                                      const uint64_t* __restrict__ pkg_pre,
+                                                      const uint16_t* __restrict__ pst_pre,
+                                                      const u32x4* __restrict__ es_pre,
+                                                      const uint64_t* __restrict__ trk_pre,
+                                                      const uint8_t* __restrict__ act_pre, uint32_t ap,
+                                                      uint32_t nw, StepArgs args) {
     extern __shared__ __align__(16) unsigned char smem[];
     const DevParams& p = args.p;
-    const uint8_t* __restrict__ actions = args.actions;
     const int* __restrict__ env_ids = args.env_ids;
     double* __restrict__ r_out = args.r_out;
-    const int fmt = args.fmt, n = args.n, auto_reset = args.auto_reset, wpb = args.wpb, lds_stride = args.lds_stride,
-              K = args.K;
+    const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride, K = args.K;
 #ifdef MDL_STAMPS
     uint64_t stamp_[16];
 #endif
     STAMP(0);
-    // The kernel arguments the loads below need, fetched in one scalar batch
-    // and pinned there (left alone, the compiler sinks each to its first use
-    // and the wave pays one dependent scalar-cache miss per argument line).
-    // The batch touches every kernarg line the step reads, so the arguments
-    // read later (constants, output pointers) hit the scalar cache.
-    int A = p.A, P = p.P, T = p.T;
-    GLOBAL const uint8_t* env_map = (GLOBAL const uint8_t*)p.env_map;
-    GLOBAL uint32_t* robp = (GLOBAL uint32_t*)p.rob;
-    GLOBAL uint64_t* pkgp = (GLOBAL uint64_t*)p.pkg;
-    GLOBAL uint16_t* pstp = (GLOBAL uint16_t*)p.pstate;
-    GLOBAL u32x4* esp = (GLOBAL u32x4*)p.es;   // EnvScalars {t, ctr, total lo, total hi}
-    GLOBAL uint64_t* trkp = (GLOBAL uint64_t*)p.trk;
-    int mW = p.maps[0].W, mgoff = p.maps[0].grid_off;
-    GLOBAL const uint8_t* actp = (GLOBAL const uint8_t*)actions;
-    GLOBAL const int* idsp = (GLOBAL const int*)env_ids;
-    int fmt_ = fmt, n_ = n, wpb_ = wpb;
-    float c_touch = p.shaping[8];
-    const uint8_t* c_touch2 = p.movevalid;
-    double* c_touch3 = r_out;
-    double c_touch4 = p.cost_sum[0], c_touch5 = p.cost_sum[8];
-    int c_touch6 = lds_stride;
-    // ONE asm statement pins them all: every load is issued before a single wait
-    // (separate pins let the compiler wait after the first few and issue the rest
-    // -- other kernarg lines, i.e. a second scalar-cache miss -- behind that wait)
-    asm volatile(""
-                 : "+s"(A), "+s"(P), "+s"(T), "+s"(env_map), "+s"(robp), "+s"(pkgp), "+s"(pstp), "+s"(esp),
-                   "+s"(trkp), "+s"(mW), "+s"(mgoff), "+s"(actp), "+s"(idsp), "+s"(fmt_), "+s"(n_), "+s"(wpb_),
-                   "+s"(c_touch), "+s"(c_touch2), "+s"(c_touch3), "+s"(c_touch4), "+s"(c_touch5), "+s"(c_touch6));
+    // Preloaded (SGPR) arguments: everything the state loads need.
+    const int A = (int)(ap & 0xffffu), P = (int)(ap >> 16);
+    const int n_ = (int)(nw & 0xffffffu), wpb_ = (int)((nw >> 24) & 31u);
+    GLOBAL const uint32_t* robp = (GLOBAL const uint32_t*)rob_pre;
+    GLOBAL const uint64_t* pkgp = (GLOBAL const uint64_t*)pkg_pre;
+    GLOBAL const uint16_t* pstp = (GLOBAL const uint16_t*)pst_pre;
+    GLOBAL const u32x4* esp = (GLOBAL const u32x4*)es_pre;   // EnvScalars {t, ctr, total lo, total hi}
+    GLOBAL const uint64_t* trkp = (GLOBAL const uint64_t*)trk_pre;
+    GLOBAL const uint8_t* actp = (GLOBAL const uint8_t*)act_pre;
     STAMP(1);
 
     const int wave = wave_id();
     const int lane = lane_id();
     const int w = blockIdx.x * wpb_ + wave;
     if (wave >= wpb_ || w >= n_) return;
-    const int e = idsp ? uni(idsp[w]) : w;
-    int mi = 0;
-    if (env_map) {
-        mi = uni(env_map[e]);
-        mW = p.maps[mi].W;
-        mgoff = p.maps[mi].grid_off;
-    }
+    const int e = (nw & NW_IDS) ? uni(((GLOBAL const int*)env_ids)[w]) : w;   // subset stepping: one more load
 
     STAMP(2);
     // ---- loads: one round trip, everything independent ----
@@ -379,6 +375,28 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
     }
     const u32x4 esv = esp[e];
     __builtin_amdgcn_sched_barrier(0);  // every load above is issued before any use
+    // The other kernel arguments, fetched now in one scalar batch while the state
+    // loads are in flight, and pinned by ONE asm statement (one wait; separate pins let
+    // the compiler wait after the first few and issue the rest behind that wait).  The
+    // batch touches every kernarg line the step reads later, so those hit the cache.
+    int T = p.T;
+    GLOBAL const uint8_t* env_map = (GLOBAL const uint8_t*)p.env_map;
+    int mW = p.maps[0].W, mgoff = p.maps[0].grid_off;
+    int fmt_ = fmt;
+    float c_touch = p.shaping[8];
+    const uint8_t* c_touch2 = p.movevalid;
+    double* c_touch3 = r_out;
+    double c_touch4 = p.cost_sum[0], c_touch5 = p.cost_sum[8];
+    int c_touch6 = lds_stride;
+    asm volatile(""
+                 : "+s"(T), "+s"(env_map), "+s"(mW), "+s"(mgoff), "+s"(fmt_), "+s"(c_touch), "+s"(c_touch2),
+                   "+s"(c_touch3), "+s"(c_touch4), "+s"(c_touch5), "+s"(c_touch6));
+    int mi = 0;
+    if (nw & NW_MAP) {
+        mi = uni(env_map[e]);
+        mW = p.maps[mi].W;
+        mgoff = p.maps[mi].grid_off;
+    }
     int cell = rob_cell(rv), carry = rob_carry(rv);
     uint32_t vmask = rob_valid(rv);
     int t_cur = (int)esv.x;
@@ -759,7 +777,8 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(StepArgs args) {
         {
             // an opaque copy of the segment pointer: the loads below cannot be hoisted
             // above this point (where their registers would have to live across the step)
-            KargPtr ka = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+            KargPtr ka = (KargPtr)((__attribute__((address_space(4))) const char*)
+                                       __builtin_amdgcn_kernarg_segment_ptr() + offsetof(StepKarg, args));
             asm volatile("" : "+s"(ka));
             rop = (GLOBAL double*)ka->r_out;
             shp = (GLOBAL float*)ka->sh_out;
@@ -1229,6 +1248,8 @@ hipError_t launch_tracker_clear(const DevParams& p, const int* ids, int n, hipSt
 template <bool ST, int NCH, bool FUSED>
 static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
                           double* r, float* sh, uint8_t* done, int wpb, size_t lds, int K, hipStream_t s) {
+    // n and wpb travel packed in one preloaded dword (n < 2^24, wpb < 32; the engine
+    // checks both at creation)
 #ifdef MDL_STEP_WPB  // profiling builds only: workgroup shape experiments
     wpb = MDL_STEP_WPB;
     const int threads = 64 * wpb;
@@ -1252,14 +1273,18 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
     a.lds_stride = (int)lds;
     a.K = K;
     const dim3 grid(blocks_for(n, wpb)), block(threads);
+    const uint32_t ap = (uint32_t)p.A | ((uint32_t)p.P << 16);
+    const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (ids ? NW_IDS : 0u) | (p.env_map ? NW_MAP : 0u);
+#define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a
     if (NCH <= 2 && p.A == 5)
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 5 : 8)>), grid, block, lds * wpb, s, a);
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 5 : 8)>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
     else if (NCH <= 2 && p.A == 16)   // config 5's robot count
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 16 : 8)>), grid, block, lds * wpb, s, a);
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, (NCH <= 2 ? 16 : 8)>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
     else if (p.A <= 8)
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 8>), grid, block, lds * wpb, s, a);
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
     else
-        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 0>), grid, block, lds * wpb, s, a);
+        hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 0>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+#undef MDL_STEP_ARGS
 }
 
 template <bool ST, bool FUSED>

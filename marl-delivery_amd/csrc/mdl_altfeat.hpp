@@ -10,14 +10,20 @@
 namespace mdl {
 
 struct AltLds {
-    uint8_t* rob;   // [HW] robot index | 0x40 if carrying; 0xff = none (robots stand on distinct cells)
-    float* urg;     // [HW] max urgency of waiting, started packages whose start is here; -1 = none
-    uint8_t* wt;    // [HW] a waiting, started package targets this cell
-    uint8_t* tt;    // [HW] an in-transit, started package targets this cell
+    uint8_t* rob;    // [HW] robot index | 0x40 if carrying; 0xff = none (robots stand on distinct cells)
+    float* urg;      // [HW] max urgency of waiting, started packages whose start is here; -1 = none
+    uint8_t* wt;     // [HW] a waiting, started package targets this cell
+    uint8_t* tt;     // [HW] an in-transit, started package targets this cell
+    uint32_t* bits;  // [ALT_NBS][NW] the same cell sets as bitsets (alt_emit_fast)
 };
 
+// bitsets of alt_emit_fast: obstacles, robots, carrying robots, waiting starts (urgency
+// >= 0), waiting targets, in-transit targets
+enum : int { ABS_GRID = 0, ABS_ROB, ABS_CARRY, ABS_START, ABS_WT, ABS_TT, ALT_NBS };
+
 __host__ __device__ inline size_t alt_lds_bytes(int HW) {
-    return align16((size_t)HW) + align16(4 * (size_t)HW) + 2 * align16((size_t)HW);
+    const size_t NW = ((size_t)HW + 31) / 32;
+    return align16((size_t)HW) + align16(4 * (size_t)HW) + 2 * align16((size_t)HW) + align16(4 * ALT_NBS * NW);
 }
 
 __device__ inline AltLds alt_carve(unsigned char* b, int HW) {
@@ -26,7 +32,8 @@ __device__ inline AltLds alt_carve(unsigned char* b, int HW) {
     L.rob = b + o; o += align16((size_t)HW);
     L.urg = (float*)(b + o); o += align16(4 * (size_t)HW);
     L.wt = b + o; o += align16((size_t)HW);
-    L.tt = b + o;
+    L.tt = b + o; o += align16((size_t)HW);
+    L.bits = (uint32_t*)(b + o);
     return L;
 }
 
@@ -68,6 +75,102 @@ __device__ inline void alt_prepare(const Trk& trk, int HW, int W, int A, int t, 
         }
     }
     wave_sync();
+}
+
+// The cell sets of alt_prepare as bitsets (two words per 64 cells, by ballot).
+__device__ inline void alt_bits(const uint32_t* gridbits, int HW, const AltLds& L) {
+    const int lane = lane_id();
+    const int NW = (HW + 31) >> 5;
+    for (int c0 = 0; c0 < HW; c0 += WAVE) {
+        const int c = c0 + lane;
+        const bool in = c < HW;
+        const uint32_t rb = in ? L.rob[c] : 0xffu;
+        const float u = in ? L.urg[c] : -1.0f;
+        const uint64_t b[ALT_NBS - 1] = {ballot(rb != 0xffu), ballot(rb != 0xffu && (rb & 0x40u)), ballot(u >= 0.0f),
+                                         ballot(in && L.wt[c]), ballot(in && L.tt[c])};
+        const int wd = c0 >> 5;
+#pragma unroll
+        for (int k = 0; k < ALT_NBS - 1; k++) {
+            // lane 2k / 2k+1 store the low / high word of set k
+            const uint32_t v = (lane & 1) ? (uint32_t)(b[k] >> 32) : (uint32_t)b[k];
+            if ((lane >> 1) == k && wd + (lane & 1) < NW) L.bits[(k + 1) * NW + wd + (lane & 1)] = v;
+        }
+    }
+    for (int k = lane; k < NW; k += WAVE) L.bits[ABS_GRID * NW + k] = gridbits[k];
+    wave_sync();
+}
+
+// Fast emission (HW % 4 == 0, 16-B aligned outputs, qmix state shape == map shape): every
+// output plane is written as float4s, float4 q of a plane being the 4 cells at 4q -- with
+// q = lane + 64k the bitset word is lane/8 + 8k at the fixed shift (lane%8)*4 -- so an
+// element costs a shift, a mask and a convert instead of a division and a branch.
+__device__ __forceinline__ float4 nib4(uint32_t nib) {
+    return make_float4((float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u), (float)(nib >> 3));
+}
+__device__ __forceinline__ uint32_t onehot_nib(int idx, int c0) {
+    const unsigned d = (unsigned)(idx - c0);
+    return d < 4u ? 1u << d : 0u;
+}
+
+// plane kinds: a bitset (or an agent-relative set), or the urgency floats
+enum : int { AP_GRID, AP_URG, AP_START, AP_OTHERS, AP_SELF, AP_TGT, AP_ROB, AP_CARRY, AP_WT, AP_TT, AP_ZERO };
+
+__device__ inline void alt_emit_plane(const AltLds& L, int NW, int HW, int kind, int self, int tgt, float* dst) {
+    const int lane = lane_id();
+    const int nq = HW >> 2;
+    const uint32_t sh = (uint32_t)(lane & 7) << 2;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    if (kind == AP_URG) {
+        const float4* u4 = reinterpret_cast<const float4*>(L.urg);
+        for (int q = lane; q < nq; q += WAVE) {
+            const float4 u = u4[q];   // -1 = no package: 0
+            d4[q] = make_float4(fmaxf(u.x, 0.0f), fmaxf(u.y, 0.0f), fmaxf(u.z, 0.0f), fmaxf(u.w, 0.0f));
+        }
+        return;
+    }
+    const int bs = kind == AP_GRID ? ABS_GRID : kind == AP_START ? ABS_START : kind == AP_CARRY ? ABS_CARRY
+                 : kind == AP_WT ? ABS_WT : kind == AP_TT ? ABS_TT : ABS_ROB;
+    const uint32_t* src = L.bits + bs * NW + (lane >> 3);
+    for (int q = lane; q < nq; q += WAVE, src += 8) {
+        const int c0 = q << 2;
+        uint32_t nib = (*src >> sh) & 15u;
+        const uint32_t so = onehot_nib(self, c0);
+        nib = kind == AP_OTHERS ? nib & ~so : kind == AP_SELF ? so : kind == AP_TGT ? onehot_nib(tgt, c0)
+            : kind == AP_ZERO ? 0u : nib;
+        d4[q] = nib4(nib);
+    }
+}
+
+template <class Trk>
+__device__ inline void alt_emit_fast(const Trk& trk, int H, int W, const AltLds& L, int cell, int carry, int A,
+                                     float* idq, float* qst) {
+    const int HW = H * W, NW = (HW + 31) >> 5;
+    if (idq) {
+        for (int a = 0; a < A; a++) {
+            const int ca = rdl(cell, a), ka = rdl(carry, a);
+            const int self = cell_r(ca) * W + cell_c(ca);
+            int tgt5 = -1;  // carried package's target, when the id is in the tracker
+            if (ka != 0) {
+                const int sl = trk.slot_of(ka);
+                if (sl >= 0) {
+                    const int tg = pk_target(trk.data(sl));
+                    tgt5 = cell_r(tg) * W + cell_c(tg);
+                }
+            }
+            float* o = idq + (size_t)a * 6 * HW;
+            alt_emit_plane(L, NW, HW, AP_GRID, self, tgt5, o);
+            alt_emit_plane(L, NW, HW, ka == 0 ? AP_URG : AP_ZERO, self, tgt5, o + HW);
+            alt_emit_plane(L, NW, HW, ka == 0 ? AP_START : AP_ZERO, self, tgt5, o + 2 * HW);
+            alt_emit_plane(L, NW, HW, AP_OTHERS, self, tgt5, o + 3 * HW);
+            alt_emit_plane(L, NW, HW, AP_SELF, self, tgt5, o + 4 * HW);
+            alt_emit_plane(L, NW, HW, AP_TGT, self, tgt5, o + 5 * HW);
+        }
+    }
+    if (qst) {
+        const int kinds[7] = {AP_GRID, AP_ROB, AP_CARRY, AP_START, AP_WT, AP_TT, AP_URG};
+#pragma unroll
+        for (int ch = 0; ch < 7; ch++) alt_emit_plane(L, NW, HW, kinds[ch], -1, -1, qst + (size_t)ch * HW);
+    }
 }
 
 // convert_state for agents [a0, a0+na): dst [na][6][H][W]

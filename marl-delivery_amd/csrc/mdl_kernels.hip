@@ -1082,10 +1082,18 @@ __global__ __launch_bounds__(256) void k_alt_obs(DevParams p, int env_begin, int
     }
     wave_sync();
     const uint8_t* grid = p.grids + md.grid_off;
+    float* idq_e = idq ? idq + (size_t)w * A * 6 * H * W : nullptr;
+    float* qst_e = qst ? qst + (size_t)w * 7 * oh * ow : nullptr;
+    const bool fast = (H * W) % 4 == 0 && oh == H && ow == W && (((uintptr_t)idq_e | (uintptr_t)qst_e) & 15) == 0;
     auto run = [&](const auto& trk) {
         alt_prepare(trk, H * W, W, A, t, cell, carry, L);
-        if (idq) alt_emit_idq(trk, grid, H, W, L, cell, carry, 0, A, true, idq + (size_t)w * A * 6 * H * W);
-        if (qst) alt_emit_qmix(grid, H, W, L, oh, ow, qst + (size_t)w * 7 * oh * ow);
+        if (fast) {
+            alt_bits(p.gridbits + md.bits_off, H * W, L);
+            alt_emit_fast(trk, H, W, L, cell, carry, A, idq_e, qst_e);
+            return;
+        }
+        if (idq) alt_emit_idq(trk, grid, H, W, L, cell, carry, 0, A, true, idq_e);
+        if (qst) alt_emit_qmix(grid, H, W, L, oh, ow, qst_e);
     };
     if (STALE) {
         TrkStale trk{S.ps, S.td, S.tq, P};

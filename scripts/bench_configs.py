@@ -5,6 +5,9 @@
   --config 3b  as 3 with the 1007-dim actor vector (MO=MP=100)
   --config 4   map1..map5 mixed, A=5, E=65536/8 per GPU (one GPU's shard), step only
   --config 5   synthetic 64x64, A=16, P=100, E=131072/8 per GPU, step only
+  --config rollout / rollout_graph   MAPPO rollout on the device
+  --config alt      IDQ/qmix featurizers (§8(f)2)
+  --config greedy   batched greedy baseline (§8(f)3)
 
 Prints one JSON line per config with per-kernel HIP-event times and the
 algorithmic-bytes roofline of SURVEY.md §8(d).
@@ -128,6 +131,54 @@ def run_rollout(steps, graph=False):
     print(json.dumps(out))
 
 
+def run_alt(steps):
+    """IDQ/qmix featurizers on 4096 map1 envs, A=5: convert_state for every
+    agent (6 x H x W) and convert_global_state_to_tensor (7 x H x W), written by one kernel."""
+    import marl_gpu
+    from marl_gpu.maps import grid_array, load_map, map_path
+    E, A, P, T, H, W = 4096, 5, 50, 500, 10, 10
+    env = marl_gpu.BatchedEnv(grid_array(load_map(map_path("map1.txt"))), E, A, P, T, seed=42, tracker="fresh")
+    env.reset()
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    for k in range(60):
+        env.step(torch.randint(0, 15, (E, A), generator=gen, device="cuda", dtype=torch.int32).to(torch.uint8))
+    out = env.build_obs_alt()
+    us = timed(lambda k: env.build_obs_alt(out=out), max(20, steps // 5))
+    nbytes = E * 4 * (A * 6 * H * W + 7 * H * W)
+    print(json.dumps({"config": "alt_featurizers", "envs": E, "agents": A, "us_per_call": us, "write_bytes": nbytes,
+                      "roofline": {"achieved_GBs": nbytes / (us * 1e-6) / 1e9, "frac": nbytes / (us * 1e-6) / 1e9 / HBM},
+                      "note": "mdl_build_obs_alt: IDQ convert_state x A + qmix convert_global_state_to_tensor"}),
+          flush=True)
+    env.close()
+
+
+def run_greedy(steps):
+    """Batched greedy baseline: 4096 map1 envs, A=5, one greedyagent.py
+    get_actions per env plus the step, per env-step (one episode, no resets)."""
+    import marl_gpu
+    from marl_gpu.maps import grid_array, load_map, map_path
+    E, A, P, T = 4096, 5, 50, 500
+    env = marl_gpu.BatchedEnv(grid_array(load_map(map_path("map1.txt"))), E, A, P, T, seed=42, tracker="fresh")
+    env.reset()
+    env.greedy_init()
+    acts = torch.empty((E, A), dtype=torch.uint8, device="cuda")
+    n = min(steps, T - 20)
+
+    def one(k):
+        env.greedy_actions(out=acts)
+        env.step(acts, auto_reset=False, action_format="codes")
+
+    for k in range(10):
+        one(k)
+    us = timed(one, n)
+    g_us = timed(lambda k: env.greedy_actions(out=acts), 20)
+    print(json.dumps({"config": "greedy", "envs": E, "agents": A, "us_per_env_step": us,
+                      "agent_steps_per_s": E * A / (us * 1e-6), "greedy_actions_us": g_us,
+                      "note": "greedy_actions (BFS distance tables precomputed per map) + mdl_step per env-step"}),
+          flush=True)
+    env.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="3,3b,4,5")
@@ -138,6 +189,10 @@ def main():
     for c in a.config.split(","):
         if c in ("rollout", "rollout_graph"):
             run_rollout(a.steps, graph=c == "rollout_graph")
+        elif c == "alt":
+            run_alt(a.steps)
+        elif c == "greedy":
+            run_greedy(a.steps)
         else:
             run(c, a.steps, a.warmup)
 

@@ -146,9 +146,10 @@ __global__ __launch_bounds__(256) void k_greedy_act(DevParams p, GreedyLayout g,
     }
     // ... and the packages of this state (spawns at t), appended in id order
     int flags = 0;
+    uint64_t pk0 = lane < P ? pk[lane] : 0;   // packages 0..63 on their lanes (for the bpermute below)
     for (int j0 = 0; j0 < P; j0 += WAVE) {
         const int j = j0 + lane;
-        const bool sp = j < P && pk_st(pk[j]) == t;
+        const bool sp = j < P && pk_st(j0 == 0 ? pk0 : pk[j]) == t;
         const uint64_t b = ballot(sp);
         const int pos = nl + popc64(b & lanemask_lt());
         if (sp && pos < cap) {
@@ -196,31 +197,36 @@ __global__ __launch_bounds__(256) void k_greedy_act(DevParams p, GreedyLayout g,
     }
     // update_move_to_target (greedyagent.py:66-102) on the robot lanes
     int mv = MV_S, op = 0;
+    // self.packages[target_package_id]: from its lane when P <= 64 (no dependent load)
+    const int tj = (act && idx >= 0) ? list[idx] - 1 : 0;
+    const uint32_t dlo = (uint32_t)__builtin_amdgcn_ds_bpermute((tj & 63) << 2, (int)(uint32_t)pk0);
+    const uint32_t dhi = (uint32_t)__builtin_amdgcn_ds_bpermute((tj & 63) << 2, (int)(uint32_t)(pk0 >> 32));
     if (act && idx >= 0) {
-        const uint64_t d = pk[list[idx] - 1];           // self.packages[target_package_id]
+        const uint64_t d = P <= WAVE ? ((uint64_t)dhi << 32 | dlo) : pk[tj];
         const int pt = phase ? pk_target(d) : pk_start(d);
         const int pr = cell_r(pt), pc = cell_c(pt), rr = cell_r(cell), rc = cell_c(cell);
         op = phase ? 2 : 1;
         if (abs(pr - rr) + abs(pc - rc) >= 1) {
             // run_bfs: distances from the goal; the first neighbour in U, D, L, R order one
-            // step closer, else 'S'; unreachable start -> ('S', 100000)
+            // step closer, else 'S'; unreachable start -> ('S', 100000).  The cell's and its
+            // neighbours' distances are loaded together (one round trip).
             const uint16_t* Dg = tables + g.tab_off[mi] + (size_t)(pr * W + pc) * HW;
             const int s = rr * W + rc;
+            const int nb[4] = {rr > 0 ? s - W : -1, rr + 1 < H ? s + W : -1, rc > 0 ? s - 1 : -1,
+                               rc + 1 < W ? s + 1 : -1};
+            int dn[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) dn[k] = Dg[nb[k] >= 0 ? nb[k] : s];
             const int ds = Dg[s];
             int d2 = 100000;
             if (ds != BFS_INF) {
                 d2 = ds;
-                const int nb[4] = {rr > 0 ? s - W : -1, rr + 1 < H ? s + W : -1, rc > 0 ? s - 1 : -1,
-                                   rc + 1 < W ? s + 1 : -1};
                 const int code[4] = {MV_U, MV_D, MV_L, MV_R};
 #pragma unroll
                 for (int k = 3; k >= 0; k--) {
-                    if (nb[k] >= 0) {
-                        const int dn = Dg[nb[k]];
-                        if (dn != BFS_INF && dn == ds - 1) {
-                            mv = code[k];
-                            d2 = dn;
-                        }
+                    if (nb[k] >= 0 && dn[k] != BFS_INF && dn[k] == ds - 1) {
+                        mv = code[k];
+                        d2 = dn[k];
                     }
                 }
             }

@@ -233,6 +233,14 @@ def test_vs_oracle_robot_counts(mapname, A, P, T):
     _oracle_compare(mapname, 32, A, P, T, 300 + A, 90, "mappo")
 
 
+@pytest.mark.parametrize("mapname,A,P,T", [("map2.txt", 8, 130, 50), ("map4.txt", 5, 300, 50),
+                                           ("synthetic64.txt", 64, 1024, 40), ("map2.txt", 3, 1024, 30)])
+def test_vs_oracle_package_chunks(mapname, A, P, T):
+    """Package tables of 2..16 register chunks (NCH = 4, 8, 16) up to MDL_MAX_PACKAGES,
+    with MDL_MAX_ROBOTS robots on the 64x64 map."""
+    _oracle_compare(mapname, 6, A, P, T, 500 + P, 45, "mappo", check_every=15)
+
+
 def test_vs_oracle_dense_synthetic():
     _oracle_compare("synthetic64.txt", 16, 16, 100, 50, 77, 120, "mappo", check_every=20)
 

@@ -275,3 +275,35 @@ def test_compat_vectorized_indices():
             r0, _, d0 = envs[i].step(mv, op)
             assert rw[j] == r0 and dn[j] == d0
             assert [r[:2] for r in st[j]["robots"]] == [tuple(x) for x in (envs[i].state()["robots"][:, :2] + 1).tolist()]
+
+
+@pytest.mark.parametrize("mapname,A,P,MO,MP", [("map4.txt", 5, 300, 4, 20), ("map2.txt", 8, 1024, 100, 100)])
+def test_obs_large_package_tables(mapname, A, P, MO, MP):
+    """The general observation builder (P > 64) up to MDL_MAX_PACKAGES vs the oracle."""
+    mg = _mg()
+    g = grid(mapname)
+    H, W = g.shape
+    E, T = 8, 60
+    env = mg.BatchedEnv(g, E, A, P, T, seed=21, tracker="mappo", max_other_robots=MO, max_packages_obs=MP)
+    env.reset()
+    ob = O.OracleBatch(E, g, A, P, T, seed_base=21, clear_on_reset=False)
+    gen = np.random.RandomState(8)
+    bufs = env.obs_buffers()
+    for k in range(25):
+        ints = gen.randint(0, 15, size=(E, A)).astype(np.uint8)
+        env.step(torch.from_numpy(ints).cuda())
+        ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS)
+        if k % 12 == 0:
+            env.build_obs(out=bufs)
+            o = {kk: v.cpu().numpy() for kk, v in bufs.items()}
+            for e in range(E):
+                oe, ot = ob.env(e), ob.tracker(e)
+                st, rb1, rows = oe.state(), oe.robots1(), ot.rows()
+                av = np.stack([O.generate_vector_features(H, W, st["t"], rb1, rows, a, T, MO, MP) for a in range(A)])
+                am = np.stack([O.convert_observation(g, st["t"], rb1, rows, a) for a in range(A)])
+                gm, gv = O.convert_global_state(g, st["t"], rb1, rows, T, 100, 100)
+                np.testing.assert_array_equal(o["actor_vec"][e], av, f"avec env {e} step {k}")
+                np.testing.assert_array_equal(o["actor_map"][e], am, f"amap env {e} step {k}")
+                np.testing.assert_array_equal(o["critic_map"][e], gm, f"cmap env {e} step {k}")
+                np.testing.assert_array_equal(o["critic_vec"][e], gv, f"cvec env {e} step {k}")
+    env.close()

@@ -540,6 +540,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
         // disjoint package sets and drops touch only carried packages: the robot
         // order of the reference loop cannot change any outcome.
         uint64_t pickers = ballot(!(MDL_ABLATE & 8) && act && op == 1 && carry == 0);
+        uint64_t tookany = 0;   // some package was picked up (the carried set changed)
         if (pickers) {
             // per robot: the lowest-index waiting package at its cell
             int sw[NCH];
@@ -564,7 +565,10 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
             }
             carry = cnew;
 #pragma unroll
-            for (int c = 0; c < NCH; c++) ps[c] = vbit(took[c], lane) ? ((ps[c] & ~PS_STATUS) | ST_IN_TRANSIT) : ps[c];
+            for (int c = 0; c < NCH; c++) {
+                ps[c] = vbit(took[c], lane) ? ((ps[c] & ~PS_STATUS) | ST_IN_TRANSIT) : ps[c];
+                tookany |= took[c];
+            }
         }
         // drops: a robot with op 2 carrying a package (its pre-step one: it did not
         // pick) and standing on that package's target delivers it
@@ -595,11 +599,14 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
         STAMP(5);
         // ---- terminate (env.py:308-316) + spawn (get_state env.py:133-137) ----
         int ndel = 0;
+        uint64_t spawned = 0;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const int j = c * WAVE + lane;
             ndel += popc64(ballot((ps[c] & PS_STATUS) == ST_DELIVERED));
-            if (j < P && pk_st(pk[c]) == t1) ps[c] = (ps[c] & ~PS_STATUS) | ST_WAITING;
+            const bool sp = j < P && pk_st(pk[c]) == t1;
+            spawned |= ballot(sp);
+            if (sp) ps[c] = (ps[c] & ~PS_STATUS) | ST_WAITING;
         }
         const bool done = (t1 == T) || (ndel == P);
 
@@ -737,7 +744,10 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
         // ---- tracker update with the new state; a done env that resets here skips
         // it and updates with the reset state instead (MAPPO/trainer.py:230-259) ----
         const bool do_rst = done && auto_reset;
-        if (STALE && !do_rst && !(MDL_ABLATE & 2)) tracker_update_regs<NCH, AU>(ps, td, dirty, pk, P, A, carry, t1);
+        // After an update, the present entries in transit are exactly the carried ones; with
+        // no pick-up, no drop and no spawn at t1 the update is a no-op, so it is skipped.
+        if (STALE && !do_rst && !(MDL_ABLATE & 2) && (tookany | dmask | spawned))
+            tracker_update_regs<NCH, AU>(ps, td, dirty, pk, P, A, carry, t1);
 
         // ---- reset on done (MAPPO/trainer.py:230-235) ----
         int t_out = t1;

@@ -356,6 +356,10 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
     uint64_t pk[NCH], td[NCH];
     uint32_t ps[NCH], ps_in[NCH], tq[NCH];
     bool dirty[NCH];
+    // the env's rows as scalar bases: each load is one SGPR base + a 32-bit lane offset
+    GLOBAL const uint64_t* pkge = pkgp + (size_t)e * P;
+    GLOBAL const uint16_t* pste = pstp + (size_t)e * P;
+    GLOBAL const uint64_t* trke = trkp + (size_t)e * P;
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
@@ -365,10 +369,9 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
         tq[c] = 0;
         dirty[c] = false;
         if (j < P) {
-            const size_t g = (size_t)e * P + j;
-            pk[c] = pkgp[g];
-            ps[c] = pstp[g];
-            if (STALE) td[c] = trkp[g];
+            pk[c] = pkge[(uint32_t)j];
+            ps[c] = pste[(uint32_t)j];
+            if (STALE) td[c] = trke[(uint32_t)j];
         }
         ps_in[c] = ps[c];
     }
@@ -470,7 +473,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
         // the proposed cell's move-validity bits, fetched now (every mover) so the load
         // overlaps the resolution below; consumed only at write-back, for robots that moved
         // (every lane loads: prop is a cell of the map on every lane, 0 on lanes >= A)
-        uint32_t pvm = (MDL_ABLATE & 16) ? vmask : (uint32_t)p.movevalid[mgoff + cell_r(prop) * mW + cell_c(prop)];
+        uint32_t pvm = (MDL_ABLATE & 16) ? vmask : (uint32_t)p.movevalid[(uint32_t)(mgoff + cell_r(prop) * mW + cell_c(prop))];
         uint64_t moved = 0;
         STAMP(12);
         if (movers) {
@@ -819,10 +822,10 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
     for (int c = 0; c < NCH; c++) {
         const int j = c * WAVE + lane;
         if (j < P) {
-            const size_t g = (size_t)e * P + j;
-            if (ps[c] != ps_in[c]) pstw[g] = (uint16_t)ps[c];
-            if (any_rst) p.pkg[g] = pk[c];
-            if (STALE && dirty[c]) trkw[g] = td[c];
+            const size_t eb = (size_t)e * P;   // uniform row base; the lane offset stays 32-bit
+            if (ps[c] != ps_in[c]) (pstw + eb)[(uint32_t)j] = (uint16_t)ps[c];
+            if (any_rst) ((GLOBAL uint64_t*)p.pkg + eb)[(uint32_t)j] = pk[c];
+            if (STALE && dirty[c]) (trkw + eb)[(uint32_t)j] = td[c];
         }
     }
     if (lane == 0)

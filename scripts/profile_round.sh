@@ -26,3 +26,8 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_obs -d $O3
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_obs -d $O3/write -o run --output-format csv -- python3 $C > $O3/write.log 2>&1 || exit $?
 python3 scripts/pmc_summary.py ${TAG}_obs k_obs > $O3/summary_obs.json || exit $?
 ls $O $O3
+# config 3b (1007-dim actor vectors): kernel trace + stats only
+O3B=$R/gpurun_out/prof_${TAG}_obs3b
+mkdir -p $O3B
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O3B/trace -o run --output-format csv -- python3 $R/scripts/bench_configs.py --config 3b > $O3B/trace.log 2>&1 || exit $?
+ls $O3B

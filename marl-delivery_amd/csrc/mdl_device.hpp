@@ -35,6 +35,7 @@ struct MapDesc {
     int rank_off;   // into rank (u16) table [(2H-1)][(2W-1)]
     float inv_hw;   // 1/(H*W) for fast divmod
     int bits_off;   // into gridbits (u32 words, ceil(H*W/32) per map)
+    int mvc_off;    // into movevalid_cell (256*W bytes per map, indexed by the packed cell r | c<<8)
 };
 
 // Per-env scalars, one 16-byte record (one load / one store per step).
@@ -70,6 +71,7 @@ struct DevParams {
     MapDesc maps[MAX_MAPS];
     const uint8_t* grids;
     const uint8_t* movevalid;  // per map cell: bit m set if move code m (L,R,U,D = 1..4) stays on a free cell
+    const uint8_t* movevalid_cell;  // the same bits indexed by the packed cell value (no r*W+c in the step)
     const uint32_t* gridbits;  // per map obstacle bitset
     const uint16_t* free_cells;
     const uint16_t* rank;

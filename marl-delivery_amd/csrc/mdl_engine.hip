@@ -168,7 +168,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     }
 
     // ---- maps ----
-    std::vector<uint8_t> allgrid, allvalid;
+    std::vector<uint8_t> allgrid, allvalid, allvalidc;
     int rank_max = 0;
     long dl_max = 0;
     std::vector<uint32_t> allbits;
@@ -190,6 +190,8 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         md.rank_off = (int)allrank.size();
         md.inv_hw = 1.0f / (float)(H * W);
         md.bits_off = (int)allbits.size();
+        md.mvc_off = (int)allvalidc.size();
+        allvalidc.resize(allvalidc.size() + (size_t)256 * W, 0);
         for (int w = 0; w < (H * W + 31) / 32; w++) {
             uint32_t b = 0;
             for (int k = 0; k < 32; k++)
@@ -211,6 +213,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
             if (r - 1 >= 0 && g[i - W] != 1) vm |= 1u << 3;
             if (r + 1 < H && g[i + W] != 1) vm |= 1u << 4;
             allvalid.push_back(vm);
+            allvalidc[(size_t)md.mvc_off + ((size_t)col << 8 | (size_t)r)] = vm;
             if (g[i] == 0) {
                 allfree.push_back((uint16_t)((i / W) | ((i % W) << 8)));
                 nf++;
@@ -289,6 +292,8 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     int rc = 0;
     rc |= eng->alloc(&d_grid, allgrid.size());
     rc |= eng->alloc(&d_valid, allvalid.size());
+    uint8_t* d_validc = nullptr;
+    rc |= eng->alloc(&d_validc, allvalidc.size());
     rc |= eng->alloc(&d_bits, allbits.size());
     rc |= eng->alloc(&d_free, allfree.size());
     rc |= eng->alloc(&d_rank, allrank.size());
@@ -319,6 +324,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     }
     if (hipMemcpy(d_grid, allgrid.data(), allgrid.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_valid, allvalid.data(), allvalid.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_validc, allvalidc.data(), allvalidc.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_bits, allbits.data(), allbits.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_free, allfree.data(), allfree.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_rank, allrank.data(), allrank.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
@@ -329,6 +335,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     }
     p.grids = d_grid;
     p.movevalid = d_valid;
+    p.movevalid_cell = d_validc;
     p.gridbits = d_bits;
     p.free_cells = d_free;
     p.rank = d_rank;

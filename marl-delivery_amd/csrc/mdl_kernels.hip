@@ -385,21 +385,20 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
     const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride, K = args.K;
     int T = p.T;
     GLOBAL const uint8_t* env_map = (GLOBAL const uint8_t*)p.env_map;
-    int mW = p.maps[0].W, mgoff = p.maps[0].grid_off;
+    int mvoff = p.maps[0].mvc_off;
     int fmt_ = fmt;
     float c_touch = p.shaping[8];
-    const uint8_t* c_touch2 = p.movevalid;
+    const uint8_t* c_touch2 = p.movevalid_cell;
     double* c_touch3 = r_out;
     double c_touch4 = p.cost_sum[0], c_touch5 = p.cost_sum[8];
     int c_touch6 = lds_stride;
     asm volatile(""
-                 : "+s"(T), "+s"(env_map), "+s"(mW), "+s"(mgoff), "+s"(fmt_), "+s"(c_touch), "+s"(c_touch2),
+                 : "+s"(T), "+s"(env_map), "+s"(mvoff), "+s"(fmt_), "+s"(c_touch), "+s"(c_touch2),
                    "+s"(c_touch3), "+s"(c_touch4), "+s"(c_touch5), "+s"(c_touch6));
     int mi = 0;
     if (nw & NW_MAP) {
         mi = uni(env_map[e]);
-        mW = p.maps[mi].W;
-        mgoff = p.maps[mi].grid_off;
+        mvoff = p.maps[mi].mvc_off;
     }
     int cell = rob_cell(rv), carry = rob_carry(rv);
     uint32_t vmask = rob_valid(rv);
@@ -465,15 +464,20 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
         // loop, checked against the oracle's literal restatement.
         const int pcell = cell, pcarry = carry;
         // bits 1..4 of vmask only: S / other moves never move; L -256, R +256, U -1, D +1
-        const int dm = mv <= MV_R ? 256 : 1;
-        const int dlt = ((vmask >> mv) & 1u) ? ((mv & 1) ? -dm : dm) : 0;
+        // the cell delta of each move code from one 64-bit table of 10-bit entries
+        // (S 0, L -256, R +256, U -1, D +1, other 0), masked by the move's validity bit
+        constexpr uint64_t DTAB = (uint64_t)(0x3ffu & (uint32_t)-256) << 10 | (uint64_t)256 << 20 |
+                                  (uint64_t)(0x3ffu & (uint32_t)-1) << 30 | (uint64_t)1 << 40;
+        const int dtab = __builtin_amdgcn_sbfe((int)(uint32_t)(DTAB >> (10 * mv)), 0, 10);
+        const int vok = __builtin_amdgcn_sbfe((int)vmask, mv, 1);   // 0 or -1
+        const int dlt = dtab & vok;
         const int prop = cell + (int)(lmask(act) & (uint32_t)dlt);   // a vector mask: no exec-masked block
         const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
         const uint64_t movers = ballot(mover);
         // the proposed cell's move-validity bits, fetched now (every mover) so the load
         // overlaps the resolution below; consumed only at write-back, for robots that moved
         // (every lane loads: prop is a cell of the map on every lane, 0 on lanes >= A)
-        uint32_t pvm = (MDL_ABLATE & 16) ? vmask : (uint32_t)p.movevalid[(uint32_t)(mgoff + cell_r(prop) * mW + cell_c(prop))];
+        uint32_t pvm = (MDL_ABLATE & 16) ? vmask : (uint32_t)(p.movevalid_cell + mvoff)[(uint32_t)prop];
         uint64_t moved = 0;
         STAMP(12);
         if (movers) {
@@ -762,7 +766,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
             if (act) {
                 cell = nc;
                 carry = 0;
-                vmask = p.movevalid[mgoff + cell_r(cell) * mW + cell_c(cell)];
+                vmask = p.movevalid_cell[(uint32_t)(mvoff + cell)];
             }
             if (STALE) survivors_at_reset<NCH>(ps, tq, P);
 #pragma unroll

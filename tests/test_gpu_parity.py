@@ -195,7 +195,7 @@ def test_notebook_kat():
 # --------------------------------------------------- GPU vs oracle, larger
 def _oracle_compare(mapname, E, A, P, T, seed, steps, tracker, check_every=10, rng_seed=0):
     mg = _mg()
-    g = grid(mapname)
+    g = grid(mapname) if isinstance(mapname, str) else mapname
     env = mg.BatchedEnv(g, E, A, P, T, seed=seed, tracker=tracker, shaping="mappo", max_packages_obs=5)
     env.reset()
     ob = O.OracleBatch(E, g, A, P, T, seed_base=seed, clear_on_reset=(tracker == "fresh"))
@@ -243,6 +243,16 @@ def test_vs_oracle_package_chunks(mapname, A, P, T):
 
 def test_vs_oracle_dense_synthetic():
     _oracle_compare("synthetic64.txt", 16, 16, 100, 50, 77, 120, "mappo", check_every=20)
+
+
+@pytest.mark.parametrize("H,W", [(3, 255), (255, 3), (2, 1)])
+def test_vs_oracle_extreme_map_shapes(H, W):
+    """Maps at the 255-row / 255-column limit (the last row / column of the packed-cell
+    move-validity table) and a 2x1 strip, 10 % random obstacles."""
+    rs = np.random.RandomState(H * 1000 + W)
+    g = (rs.rand(H, W) < 0.1).astype(np.uint8) if H * W > 2 else np.zeros((H, W), np.uint8)
+    A = 5 if H * W > 2 else 1
+    _oracle_compare(g, 8, A, 40, 60, 900 + H, 80, "mappo", check_every=20)
 
 
 def test_vs_oracle_crowded():

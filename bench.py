@@ -11,7 +11,9 @@ device (Philox, seed 0) -- inputs resident in HBM before the timed region.
 A "step" = one ``mdl_step`` over all local envs.  The K timed steps are
 replayed from hipGraphs of G steps each (launch-bound loop; the same kernels
 as eager launches).  value = agent-steps/s over all ranks (weak scaling: 4096
-envs per GPU, no collective on the step path).
+envs per GPU, no collective on the step path; ``--total-envs N`` splits N envs
+over the ranks instead: strong scaling, SURVEY.md 8(e), global env ids and seeds
+unchanged).
 
 Extra fields: eager (un-captured) throughput, the roofline record of the step
 kernel (HIP-event timed), and the CPU baseline (the oracle's C restatement,
@@ -43,6 +45,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--total-envs", type=int, default=0,
+                    help="strong scaling: this many envs in total, split over the ranks (0 = weak: --envs per GPU)")
     ap.add_argument("--map", default="map1.txt")
     ap.add_argument("--agents", type=int, default=5)
     ap.add_argument("--packages", type=int, default=50)
@@ -117,8 +121,15 @@ def main():
     import marl_gpu
     from marl_gpu.maps import grid_array, load_map, map_path
     grid = grid_array(load_map(map_path(args.map)))
-    E, A, P = args.envs, args.agents, args.packages
-    seed0 = args.seed + rank * E                                  # global env index -> seed
+    A, P = args.agents, args.packages
+    if args.total_envs > 0:   # strong scaling: the ranks split one batch (lower ranks take the remainder)
+        q, rem = divmod(args.total_envs, world)
+        E = q + (1 if rank < rem else 0)
+        first = rank * q + min(rank, rem)
+        E_all = args.total_envs
+    else:
+        E, first, E_all = args.envs, rank * args.envs, args.envs * world
+    seed0 = args.seed + first                                     # global env index -> seed
     env = marl_gpu.BatchedEnv(grid, E, A, P, args.T, seed=seed0, tracker="mappo", shaping="mappo",
                               max_packages_obs=5, device=dev)
     env.reset()
@@ -226,7 +237,7 @@ def main():
         wall_eager = float(t[1]) if wall_eager is not None else None
         wall_f = float(t[2]) if wall_f is not None else None
 
-    total_agent_steps = E * A * K * world
+    total_agent_steps = E_all * A * K
     value = total_agent_steps / wall
     if rank == 0:
         per_launch_bytes = STEP_BYTES_PER_ENV(A, P) * E
@@ -253,14 +264,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": wall / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.total_envs > 0 else "weak",
             "vs_baseline": None,
             "dtype": "int32+fp64",
             "data": "synthetic: uniform random trainer-int actions (Philox, on device), env seeds 42+global index",
             "config": {"workload": f"{args.map} A={A} P={P} T={args.T} {E} envs/GPU, mdl_step "
                                    "(move+packages+env reward+MAPPO shaped reward+tracker+auto-reset), "
                                    + ("eager launches" if graph is None else "hipGraph replay"),
-                       "envs_per_gpu": E, "agents": A, "packages": P, "max_time_steps": args.T,
+                       "envs_per_gpu": E, "total_envs": E_all, "agents": A, "packages": P, "max_time_steps": args.T,
                        "parallelism": f"env-shard x{world}"},
             "gpu_event_ms_per_step": gpu_ms / K,
             "eager": None if wall_eager is None else {"value": total_agent_steps / wall_eager,
@@ -271,7 +282,7 @@ def main():
                          "kernel_us_isolated_event_pair": kdur_iso_us,
                          "algorithmic_bytes_per_launch": per_launch_bytes},
             "fused_bench_mode": None if wall_f is None else {
-                "k_steps_per_launch": Kf, "launches": nf, "value": E * A * Kf * nf * world / wall_f,
+                "k_steps_per_launch": Kf, "launches": nf, "value": E_all * A * Kf * nf / wall_f,
                 "ms_per_step": wall_f / (Kf * nf) * 1e3,
                 "note": "SURVEY.md 8(d)(ii) bench mode: mdl_step_fused, K steps per launch on pre-generated device "
                         "actions (bit-exact with K mdl_step calls); not the API path, not the headline value"},

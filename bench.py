@@ -122,14 +122,15 @@ def main():
     from marl_gpu.maps import grid_array, load_map, map_path
     grid = grid_array(load_map(map_path(args.map)))
     A, P = args.agents, args.packages
+    from marl_gpu import dist as D
     if args.total_envs > 0:   # strong scaling: the ranks split one batch (lower ranks take the remainder)
-        q, rem = divmod(args.total_envs, world)
-        E = q + (1 if rank < rem else 0)
-        first = rank * q + min(rank, rem)
+        ids, _ = D.shard_strong(args.total_envs, rank, world, args.seed)
         E_all = args.total_envs
     else:
-        E, first, E_all = args.envs, rank * args.envs, args.envs * world
-    seed0 = args.seed + first                                     # global env index -> seed
+        ids, _ = D.shard(args.envs, rank, args.seed)
+        E_all = args.envs * world
+    E = len(ids)
+    seed0 = args.seed + ids[0]                                    # global env index -> seed (contiguous ids)
     env = marl_gpu.BatchedEnv(grid, E, A, P, args.T, seed=seed0, tracker="mappo", shaping="mappo",
                               max_packages_obs=5, device=dev)
     env.reset()

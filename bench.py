@@ -130,6 +130,8 @@ def main():
         ids, _ = D.shard(args.envs, rank, args.seed)
         E_all = args.envs * world
     E = len(ids)
+    if E == 0:
+        raise SystemExit(f"bench.py: rank {rank} has no envs (--total-envs {args.total_envs} < {world} ranks)")
     seed0 = args.seed + ids[0]                                    # global env index -> seed (contiguous ids)
     env = marl_gpu.BatchedEnv(grid, E, A, P, args.T, seed=seed0, tracker="mappo", shaping="mappo",
                               max_packages_obs=5, device=dev)

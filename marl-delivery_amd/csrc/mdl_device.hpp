@@ -556,20 +556,23 @@ __device__ inline float np_sum_lanes(float v, int n) {
 // np_sum_lanes for n <= AU <= 7 as a DPP chain: lane i adds lane i-1's running sum
 // (row_shr:1) to its own value, so lane AU-1 ends with (((0 + x0) + x1) + ...) + x[AU-1]
 // in the reference's order (x + y == y + x exactly).  Lanes n..AU-1 must hold +0.0f
-// (exact: no partial sum is -0.0f).  No readlanes, no SGPRs held.
+// (exact: no partial sum is -0.0f), and no lane may hold -0.0f: then the reference's
+// leading and trailing 0.0f + x are identities and are left out.  No readlanes, no
+// SGPRs held.
 template <int AU>
 __device__ inline float np_sum_lanes_dpp(float v) {
     static_assert(AU >= 1 && AU <= 7, "np_sum_lanes_dpp: 1 <= AU <= 7");
-    float t = 0.0f + v;
+    float t = v;
 #pragma unroll
     for (int i = 1; i < AU; i++) {
         const float prev = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), 0x111, 0xf, 0xf, true));
         t = v + prev;
     }
-    return 0.0f + rdlf(t, AU - 1);
+    return rdlf(t, AU - 1);
 }
 
 // the step kernel's sum: unrolled form for AU > 0 robots, the general one otherwise
+// (the step kernel's lane values are sums or masked +0.0f: never -0.0f)
 template <int AU>
 __device__ inline float np_sum_step(float v, int n) {
     if constexpr (AU > 0 && AU <= 7) return np_sum_lanes_dpp<AU>(v);

@@ -737,8 +737,8 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
             const float t4v = fmask(Mt & lmask(da < db), cs[SH_CLOSER]) + fmask(Mt & lmask(da > db), cs[SH_AWAY]);
             // 4. idle next to an available package
             const float t5v = fmask(~Mmov & MS & Mpc0 & Midle, cs[SH_IDLE]);
-            float s = 0.0f;
-            s = s + t1v;
+            // (0.0f + t1v == t1v: t1v is a sum of two terms of which one is +0, so never -0)
+            float s = t1v;
             s = s + t2v;
             s = s + t3v;
             s = s + t4v;

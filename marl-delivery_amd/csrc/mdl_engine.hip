@@ -103,18 +103,33 @@ struct MdlEngine {
     int maxHW = 0;
     bool seeded = false;
     uint64_t map_fp = 0;  // FNV-1a of every map's (H, W, cells, env_map): checkpoint compatibility
+    uint64_t cfg_fp = 0;  // FNV-1a of the reward / shaping constants and observation dims: checkpoint compatibility
+    // shape_run_end[e]: end (exclusive) of env e's run of consecutive envs whose maps share one
+    // (H, W); an observation range must lie inside one run (its output tensors have one shape)
+    std::vector<int32_t> shape_run_end;
     // greedy baseline (mdl_greedy_*): BFS tables per map and one agent record per env, made on first use
     uint16_t* gtab = nullptr;
     unsigned char* gstate = nullptr;
     mdl::GreedyLayout glay{};
+    bool greedy_stale = false;  // set by loading a checkpoint that has no greedy section
 
     // (device pointer, bytes) of every state buffer, in checkpoint order
-    std::vector<std::pair<void*, size_t>> state_sections() const {
+    // (the greedy agents' records follow when with_greedy: they exist once mdl_greedy_init ran)
+    std::vector<std::pair<void*, size_t>> state_sections(bool with_greedy) const {
         const size_t E = p.E, A = p.A, P = p.P;
-        return {{p.rob, E * A * 4},   {p.pkg, E * P * 8},     {p.pstate, E * P * 2},
-                {p.es, E * 16},       {p.mt, E * mdl::MT_N * 4}, {p.mt_pos, E * 4},
-                {p.trk, p.stale ? E * P * 8 : 0}, {p.ep_total, E * 8}, {p.ep_len, E * 4}};
+        std::vector<std::pair<void*, size_t>> v = {
+            {p.rob, E * A * 4},   {p.pkg, E * P * 8},        {p.pstate, E * P * 2},
+            {p.es, E * 16},       {p.mt, E * mdl::MT_N * 4}, {p.mt_pos, E * 4},
+            {p.trk, p.stale ? E * P * 8 : 0}, {p.ep_total, E * 8}, {p.ep_len, E * 4}};
+        if (with_greedy) v.push_back({gstate, E * (size_t)greedy_stride()});
+        return v;
     }
+    // bytes per env of the greedy agent record (the layout greedy_alloc sets up)
+    int greedy_stride() const {
+        const int cap = 3 * p.P + 64, list_off = (8 + 4 * p.A + 3) & ~3;
+        return (list_off + 2 * cap + cap + 15) & ~15;
+    }
+    bool has_greedy() const { return gstate != nullptr && !greedy_stale; }
 
     template <class T>
     int alloc(T** ptr, size_t count) {
@@ -353,6 +368,22 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         for (uint8_t v : allgrid) mix(v);
         for (uint8_t v : em) mix(v);
         eng->map_fp = h;
+        h = 1469598103934665603ull;
+        auto mixd = [&mix](double d) { uint64_t v; memcpy(&v, &d, 8); mix(v); };
+        mixd(c.move_cost);
+        mixd(c.delivery_reward);
+        mixd(c.delay_reward);
+        for (int i = 0; i < 9; i++) mixd(c.shaping[i]);
+        mix((uint64_t)(uint32_t)c.obs_max_time_steps);
+        mix(((uint64_t)(uint32_t)c.max_other_robots << 32) | (uint32_t)c.max_packages_obs);
+        mix(((uint64_t)(uint32_t)c.max_robots_state << 32) | (uint32_t)c.max_packages_state);
+        eng->cfg_fp = h;
+    }
+    eng->shape_run_end.assign(c.n_envs, c.n_envs);
+    for (int e = c.n_envs - 2; e >= 0; e--) {
+        const int m0 = env_map ? env_map[e] : 0, m1 = env_map ? env_map[e + 1] : 0;
+        const bool same = eng->mapH[m0] == eng->mapH[m1] && eng->mapW[m0] == eng->mapW[m1];
+        eng->shape_run_end[e] = same ? eng->shape_run_end[e + 1] : e + 1;
     }
 
     eng->lds_step = mdl::step_lds((int)P);
@@ -452,6 +483,34 @@ int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format
 }
 
 // ---- greedy baseline ----
+namespace {
+// BFS tables per map and the per-env agent records, made on first use (or by a checkpoint load)
+int greedy_alloc(MdlEngine* eng, hipStream_t s) {
+    if (eng->gtab) return 0;
+    mdl::GreedyLayout& g = eng->glay;
+    g.A = eng->p.A;
+    g.cap = 3 * eng->p.P + 64;
+    g.list_off = (8 + 4 * g.A + 3) & ~3;
+    g.free_off = g.list_off + 2 * g.cap;
+    g.stride = eng->greedy_stride();
+    g.lds_stride = (3 * g.cap + 15) & ~15;
+    if (4 * (size_t)g.lds_stride > LDS_BUDGET) return fail("mdl_greedy_init: too many packages for the greedy agent");
+    int64_t tab = 0;
+    for (int m = 0; m < eng->p.n_maps; m++) {
+        const int64_t hw = (int64_t)eng->mapH[m] * eng->mapW[m];
+        if (hw > 4096) return fail("mdl_greedy_init: map %d has %lld cells (the BFS tables need <= 4096)", m,
+                                   (long long)hw);
+        g.tab_off[m] = tab;
+        tab += hw * hw;
+    }
+    if (eng->alloc(&eng->gtab, (size_t)tab) || eng->alloc(&eng->gstate, (size_t)eng->p.E * g.stride)) return -1;
+    for (int m = 0; m < eng->p.n_maps; m++)
+        HIPCHK(mdl::launch_bfs_table(eng->p.grids + eng->p.maps[m].grid_off, eng->mapH[m], eng->mapW[m],
+                                     eng->gtab + g.tab_off[m], s));
+    return 0;
+}
+}  // namespace
+
 int mdl_greedy_init(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream) {
     if (!eng) return fail("mdl_greedy_init: null engine");
     if (!eng->seeded) return fail("mdl_greedy_init: engine not seeded");
@@ -459,36 +518,19 @@ int mdl_greedy_init(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* str
     if (n < 0 || n > eng->p.E) return fail("mdl_greedy_init: n=%d out of range", n);
     DeviceGuard dg(eng->device);
     hipStream_t s = (hipStream_t)stream;
-    if (!eng->gtab) {
-        mdl::GreedyLayout& g = eng->glay;
-        g.A = eng->p.A;
-        g.cap = 3 * eng->p.P + 64;
-        g.list_off = (8 + 4 * g.A + 3) & ~3;
-        g.free_off = g.list_off + 2 * g.cap;
-        g.stride = (g.free_off + g.cap + 15) & ~15;
-        g.lds_stride = (3 * g.cap + 15) & ~15;
-        if (4 * (size_t)g.lds_stride > LDS_BUDGET) return fail("mdl_greedy_init: too many packages for the greedy agent");
-        int64_t tab = 0;
-        for (int m = 0; m < eng->p.n_maps; m++) {
-            const int64_t hw = (int64_t)eng->mapH[m] * eng->mapW[m];
-            if (hw > 4096) return fail("mdl_greedy_init: map %d has %lld cells (the BFS tables need <= 4096)", m,
-                                       (long long)hw);
-            g.tab_off[m] = tab;
-            tab += hw * hw;
-        }
-        if (eng->alloc(&eng->gtab, (size_t)tab) || eng->alloc(&eng->gstate, (size_t)eng->p.E * g.stride)) return -1;
-        for (int m = 0; m < eng->p.n_maps; m++)
-            HIPCHK(mdl::launch_bfs_table(eng->p.grids + eng->p.maps[m].grid_off, eng->mapH[m], eng->mapW[m],
-                                         eng->gtab + g.tab_off[m], s));
-    }
+    if (greedy_alloc(eng, s)) return -1;
     if (n == 0) return 0;
     HIPCHK(mdl::launch_greedy_init(eng->p, eng->glay, eng->gstate, env_ids, n, s));
+    if (!env_ids) eng->greedy_stale = false;
     return 0;
 }
 
 int mdl_greedy_actions(MdlEngine* eng, const int32_t* env_ids, int32_t n, uint8_t* actions, void* stream) {
     if (!eng || !actions) return fail("mdl_greedy_actions: null argument");
     if (!eng->gstate) return fail("mdl_greedy_actions: call mdl_greedy_init first");
+    if (eng->greedy_stale)
+        return fail("mdl_greedy_actions: the greedy agents' state predates mdl_load_state of a checkpoint without "
+                    "it; call mdl_greedy_init");
     if (!env_ids) n = eng->p.E;
     if (n < 0 || n > eng->p.E) return fail("mdl_greedy_actions: n=%d out of range", n);
     if (n == 0) return 0;
@@ -500,20 +542,28 @@ int mdl_greedy_actions(MdlEngine* eng, const int32_t* env_ids, int32_t n, uint8_
 
 // ---- checkpoint ----
 namespace {
+constexpr uint32_t CKPT_VERSION = 2;
+constexpr uint32_t CKPT_GREEDY = 1u;  // flags: the greedy agents' records follow the env state
 struct CkptHeader {
     char magic[8];  // "MDLSTATE"
     uint32_t version, tracker_mode;
     int32_t E, A, P, T, n_maps, seeded;
     uint64_t map_fp, payload_bytes;
+    uint64_t cfg_fp;  // reward / shaping constants, observation dims
+    uint32_t flags, reserved;
 };
-static_assert(sizeof(CkptHeader) == 56, "checkpoint header layout");
+static_assert(sizeof(CkptHeader) == 72, "checkpoint header layout");
+
+size_t payload(const MdlEngine* eng, bool with_greedy) {
+    size_t n = 0;
+    for (auto& s : eng->state_sections(with_greedy)) n += s.second;
+    return n;
+}
 }  // namespace
 
 int mdl_state_bytes(MdlEngine* eng, int64_t* bytes) {
     if (!eng || !bytes) return fail("mdl_state_bytes: null argument");
-    size_t n = sizeof(CkptHeader);
-    for (auto& s : eng->state_sections()) n += s.second;
-    *bytes = (int64_t)n;
+    *bytes = (int64_t)(sizeof(CkptHeader) + payload(eng, eng->has_greedy()));
     return 0;
 }
 
@@ -524,18 +574,21 @@ int mdl_save_state(MdlEngine* eng, void* buf, int64_t bytes, void* stream) {
                                           (long long)need);
     DeviceGuard dg(eng->device);
     hipStream_t s = (hipStream_t)stream;
+    const bool g = eng->has_greedy();
     CkptHeader h{};
     memcpy(h.magic, "MDLSTATE", 8);
-    h.version = 1;
+    h.version = CKPT_VERSION;
     h.tracker_mode = (uint32_t)eng->cfg.tracker_mode;
     h.E = eng->p.E; h.A = eng->p.A; h.P = eng->p.P; h.T = eng->p.T;
     h.n_maps = eng->p.n_maps;
     h.seeded = eng->seeded ? 1 : 0;
     h.map_fp = eng->map_fp;
-    h.payload_bytes = (uint64_t)(need - (int64_t)sizeof(CkptHeader));
+    h.cfg_fp = eng->cfg_fp;
+    h.flags = g ? CKPT_GREEDY : 0u;
+    h.payload_bytes = (uint64_t)payload(eng, g);
     memcpy(buf, &h, sizeof h);
     char* o = (char*)buf + sizeof h;
-    for (auto& sec : eng->state_sections()) {
+    for (auto& sec : eng->state_sections(g)) {
         if (sec.second) HIPCHK(hipMemcpyAsync(o, sec.first, sec.second, hipMemcpyDeviceToHost, s));
         o += sec.second;
     }
@@ -544,27 +597,38 @@ int mdl_save_state(MdlEngine* eng, void* buf, int64_t bytes, void* stream) {
 }
 
 int mdl_load_state(MdlEngine* eng, const void* buf, int64_t bytes, void* stream) {
-    int64_t need = 0;
-    if (mdl_state_bytes(eng, &need)) return -1;
+    if (!eng) return fail("mdl_load_state: null engine");
     if (!buf || bytes < (int64_t)sizeof(CkptHeader)) return fail("mdl_load_state: truncated checkpoint");
     CkptHeader h;
     memcpy(&h, buf, sizeof h);
-    if (memcmp(h.magic, "MDLSTATE", 8) != 0 || h.version != 1) return fail("mdl_load_state: not an engine checkpoint");
+    if (memcmp(h.magic, "MDLSTATE", 8) != 0) return fail("mdl_load_state: not an engine checkpoint");
+    if (h.version != CKPT_VERSION)
+        return fail("mdl_load_state: checkpoint version %u, this engine reads version %u", h.version, CKPT_VERSION);
     if (h.E != eng->p.E || h.A != eng->p.A || h.P != eng->p.P || h.T != eng->p.T ||
         h.tracker_mode != (uint32_t)eng->cfg.tracker_mode || h.n_maps != eng->p.n_maps || h.map_fp != eng->map_fp)
         return fail("mdl_load_state: checkpoint of a different configuration (E=%d A=%d P=%d T=%d, maps %llx)", h.E, h.A,
                     h.P, h.T, (unsigned long long)h.map_fp);
+    if (h.cfg_fp != eng->cfg_fp)
+        return fail("mdl_load_state: checkpoint of an engine with other reward / shaping constants or observation "
+                    "dimensions");
+    if (h.flags & ~CKPT_GREEDY) return fail("mdl_load_state: unknown checkpoint flags %#x", h.flags);
+    const bool g = (h.flags & CKPT_GREEDY) != 0;
+    const int64_t need = (int64_t)(sizeof h + payload(eng, g));
     if (bytes < need || h.payload_bytes != (uint64_t)(need - (int64_t)sizeof h))
         return fail("mdl_load_state: checkpoint of %lld bytes, need %lld", (long long)bytes, (long long)need);
     DeviceGuard dg(eng->device);
     hipStream_t s = (hipStream_t)stream;
+    if (g && greedy_alloc(eng, s)) return -1;
     const char* in = (const char*)buf + sizeof h;
-    for (auto& sec : eng->state_sections()) {
+    for (auto& sec : eng->state_sections(g)) {
         if (sec.second) HIPCHK(hipMemcpyAsync(sec.first, in, sec.second, hipMemcpyHostToDevice, s));
         in += sec.second;
     }
     HIPCHK(hipStreamSynchronize(s));
     eng->seeded = h.seeded != 0;
+    // greedy records not in the checkpoint describe the engine's pre-load episodes: refuse them
+    eng->greedy_stale = !g && eng->gstate != nullptr;
+    if (g) eng->greedy_stale = false;
     return 0;
 }
 
@@ -573,6 +637,9 @@ int mdl_build_obs(MdlEngine* eng, int32_t env_begin, int32_t n, float* actor_map
     if (!eng) return fail("mdl_build_obs: null engine");
     if (env_begin < 0 || n < 0 || env_begin + n > eng->p.E) return fail("mdl_build_obs: env range out of bounds");
     if (n == 0) return 0;
+    if (eng->shape_run_end[env_begin] < env_begin + n)
+        return fail("mdl_build_obs: envs [%d, %d) mix map shapes (same-shape run ends at %d)", env_begin,
+                    env_begin + n, eng->shape_run_end[env_begin]);
     DeviceGuard dg(eng->device);
     HIPCHK(mdl::launch_obs(eng->p, env_begin, n, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs,
                            eng->lds_obs, (hipStream_t)stream));
@@ -630,6 +697,9 @@ int mdl_build_obs_alt(MdlEngine* eng, int32_t env_begin, int32_t n, float* idq_o
     if (qmix_state && (out_h < 1 || out_w < 1 || out_h > 4096 || out_w > 4096))
         return fail("mdl_build_obs_alt: bad state tensor shape (%d, %d)", out_h, out_w);
     if (n == 0) return 0;
+    if (eng->shape_run_end[env_begin] < env_begin + n)
+        return fail("mdl_build_obs_alt: envs [%d, %d) mix map shapes (same-shape run ends at %d)", env_begin,
+                    env_begin + n, eng->shape_run_end[env_begin]);
     const size_t lds = mdl::alt_obs_lds(eng->p.P, eng->maxHW);
     const int wpb = waves_per_block(lds);
     if (wpb < 1) return fail("mdl_build_obs_alt: needs %zu bytes of LDS per env", lds);

@@ -99,6 +99,7 @@ __global__ __launch_bounds__(256) void k_greedy_init(DevParams p, GreedyLayout g
     const int w = blockIdx.x * 4 + wave_id();
     if (w >= n) return;
     const int e = env_ids ? env_ids[w] : w;
+    if ((unsigned)e >= (unsigned)p.E) return;
     const int lane = lane_id();
     GreedyRec R = greedy_rec(gs, g, e);
     if (lane < p.A) {
@@ -123,6 +124,7 @@ __global__ __launch_bounds__(256) void k_greedy_act(DevParams p, GreedyLayout g,
     const int w = blockIdx.x * 4 + wave;
     if (w >= n) return;
     const int e = env_ids ? env_ids[w] : w;
+    if ((unsigned)e >= (unsigned)p.E) return;
     const int lane = lane_id();
     const int A = p.A, P = p.P, cap = g.cap;
     uint16_t* list = (uint16_t*)(smem + (size_t)wave * g.lds_stride);

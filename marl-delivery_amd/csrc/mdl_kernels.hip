@@ -217,6 +217,7 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restric
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
     const int e = env_ids ? env_ids[w] : w;
+    if ((unsigned)e >= (unsigned)p.E) return;  // device-side ids: out of range -> skipped
     const int A = p.A, P = p.P;
     ResetLds L = reset_carve(smem + (size_t)wave * lds_stride, P);
     const MapDesc md = p.maps[p.env_map ? p.env_map[e] : 0];
@@ -266,6 +267,7 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
     const int w = blockIdx.x * 4 + wave;
     if (w >= n) return;
     const int e = env_ids ? env_ids[w] : w;
+    if ((unsigned)e >= (unsigned)p.E) return;
     for (int j = lane_id(); j < p.P; j += WAVE) {
         const size_t g = (size_t)e * p.P + j;
         p.pstate[g] &= (uint16_t)PS_STATUS;
@@ -346,7 +348,11 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
     const int lane = lane_id();
     const int w = blockIdx.x * wpb_ + wave;
     if (wave >= wpb_ || w >= n_) return;
-    const int e = (nw & NW_IDS) ? uni(((GLOBAL const int*)args.env_ids)[w]) : w;   // subset stepping: one more load
+    int e = w;
+    if (nw & NW_IDS) {   // subset stepping: one more load; an id outside [0, E) is skipped
+        e = uni(((GLOBAL const int*)args.env_ids)[w]);
+        if ((unsigned)e >= (unsigned)args.p.E) return;
+    }
 
     STAMP(2);
     // ---- loads: one round trip, everything independent ----

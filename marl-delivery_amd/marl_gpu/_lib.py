@@ -118,3 +118,14 @@ def ptr(t) -> int | None:
 def stream_handle(device=None) -> int:
     import torch
     return torch.cuda.current_stream(device).cuda_stream
+
+
+_raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def raw_stream(index: int) -> int:
+    """hipStream_t of torch's current stream on device ``index`` (the fast accessor
+    when this torch build has it: no Stream object per call)."""
+    if _raw is not None:
+        return _raw(index)
+    return torch.cuda.current_stream(index).cuda_stream

@@ -16,6 +16,8 @@ Differences (documented, not silent):
 """
 from __future__ import annotations
 
+import operator
+
 import numpy as np
 import torch
 
@@ -213,33 +215,77 @@ class VectorizedEnv:
         for env in self.envs:
             env._refresh(snap)
 
+    def _index(self, indices):
+        """``self.envs[i]`` semantics of the reference's loops: negatives count from the
+        end, anything else out of range raises IndexError."""
+        n = self.num_envs
+        out = []
+        for i in indices:
+            i = operator.index(i)
+            if i < -n or i >= n:
+                raise IndexError("list index out of range")
+            out.append(i % n)
+        return out
+
+    @staticmethod
+    def _rounds(idx):
+        """Split positions into launches with distinct envs: the k-th occurrence of an env
+        goes to launch k, so repeated envs step (or reset) in list order, as the
+        reference's serial loop does (QMIX/env_vectorized.py:13-37)."""
+        seen, rounds = {}, []
+        for pos, e in enumerate(idx):
+            k = seen.get(e, 0)
+            seen[e] = k + 1
+            if k == len(rounds):
+                rounds.append([])
+            rounds[k].append(pos)
+        return rounds
+
     def reset(self, indices=None):
-        idx = list(range(self.num_envs)) if indices is None else list(indices)
-        self.engine.reset(None if indices is None else idx)
-        self._refresh_all()
-        return [self.envs[i]._state_dict() for i in idx]
+        if indices is None:
+            self.engine.reset(None)
+            self._refresh_all()
+            return [env._state_dict() for env in self.envs]
+        idx = self._index(indices)
+        out = [None] * len(idx)
+        for rnd in self._rounds(idx):
+            self.engine.reset([idx[p] for p in rnd])
+            self._refresh_all()
+            for p in rnd:
+                out[p] = self.envs[idx[p]]._state_dict()
+        return out
 
     def step(self, actions, indices=None):
-        idx = list(range(self.num_envs)) if indices is None else list(indices)
-        if len(actions) != len(idx):
-            raise ValueError("one action list per stepped env")
-        codes = np.stack([encode_actions(a, self.envs[i].n_robots) for i, a in zip(idx, actions)])
+        # zip() semantics of the reference (QMIX/env_vectorized.py:32-35): the shorter of
+        # the env list and the action list decides how many envs step
+        actions = list(actions)
+        if indices is None:
+            idx = list(range(min(self.num_envs, len(actions))))
+            rounds = [list(range(len(idx)))]
+            full = len(idx) == self.num_envs
+        else:
+            idx = self._index(indices)[:len(actions)]
+            rounds = self._rounds(idx)
+            full = False
         eng = self.engine
-        a = torch.from_numpy(codes).to(eng.device)
-        r, _, d = eng.step(a, env_ids=None if indices is None else idx, auto_reset=False, action_format="codes")
-        r_h = r.cpu().numpy()
-        d_h = d.cpu().numpy().astype(bool)
-        self._refresh_all()
-        states, rewards, dones, infos = [], [], [], []
-        for k, i in enumerate(idx):
-            env = self.envs[i]
-            states.append(env._state_dict())
-            rewards.append(0 if r_h[k] == 0.0 else float(r_h[k]))
-            dones.append(bool(d_h[k]))
-            info = {}
-            if d_h[k]:
-                info = {"total_reward": env.total_reward, "total_time_steps": env.t}
-            infos.append(info)
+        res = [None] * len(idx)
+        for rnd in rounds:
+            ids = [idx[p] for p in rnd]
+            codes = np.stack([encode_actions(actions[p], self.envs[e].n_robots) for p, e in zip(rnd, ids)])
+            a = torch.from_numpy(codes).to(eng.device)
+            r, _, d = eng.step(a, env_ids=None if full else ids, auto_reset=False, action_format="codes")
+            r_h = r.cpu().numpy()
+            d_h = d.cpu().numpy().astype(bool)
+            self._refresh_all()
+            for k, (p, e) in enumerate(zip(rnd, ids)):
+                env = self.envs[e]
+                info = {}
+                if d_h[k]:
+                    info = {"total_reward": env.total_reward, "total_time_steps": env.t}
+                res[p] = (env._state_dict(), 0 if r_h[k] == 0.0 else float(r_h[k]), bool(d_h[k]), info)
+        if not res:
+            raise ValueError("not enough values to unpack (expected 4, got 0)")   # zip(*[]) in the reference
+        states, rewards, dones, infos = (list(x) for x in zip(*res))
         return states, rewards, dones, infos
 
     def render(self, indices=None):

@@ -21,6 +21,7 @@ import torch
 
 from . import _lib
 from ._lib import check, lib, ptr, stream_handle
+from ._lib import raw_stream as _raw_stream
 from .maps import grid_array, load_map, map_path
 
 # shaping constants, order: pickup, on_time, late, closer, wasted_pick,
@@ -118,6 +119,14 @@ class BatchedEnv:
         self._r = torch.zeros(self.E, dtype=torch.float64, device=self.device)
         self._sh = torch.zeros(self.E, dtype=torch.float32, device=self.device)
         self._done = torch.zeros(self.E, dtype=torch.uint8, device=self.device)
+        self._fn_step = lib().mdl_step
+        self._out_ok = None
+        # end (exclusive) of each env's run of consecutive envs with the same map shape:
+        # an observation range must lie inside one run (its tensors have one H x W)
+        hw_env = np.array([self.grids[m].shape for m in self.env_map], np.int64).reshape(self.E, 2)
+        brk = np.nonzero(np.any(hw_env[1:] != hw_env[:-1], axis=1))[0] + 1
+        ends = np.append(brk, self.E)
+        self._shape_run_end = np.repeat(ends, np.diff(np.concatenate(([0], ends))))
 
     # ------------------------------------------------------------------ core
     def close(self):
@@ -135,21 +144,79 @@ class BatchedEnv:
         return C.c_void_p(stream_handle(self.device))
 
     def _ids(self, env_ids):
+        """Env-id subset -> (int32 device tensor or None, count).
+
+        Host-side ids (list / numpy / CPU tensor) are checked like the reference's
+        ``self.envs[i]`` indexing: negatives count from the end, anything outside
+        [-E, E) raises IndexError.  Duplicates raise ValueError (one launch steps
+        every listed env once, in parallel; ``compat.VectorizedEnv`` splits repeated
+        ids into sequential launches as the reference's loop does).  Device tensors
+        are taken as they are, without a host round trip: their ids must be unique
+        and in [0, E) (the kernels skip ids outside that range, so a bad id cannot
+        touch another env's memory, but it is not reported)."""
         if env_ids is None:
             return None, self.E
-        ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).contiguous()
-        return ids, int(ids.numel())
+        if isinstance(env_ids, torch.Tensor) and env_ids.is_cuda:
+            ids = env_ids
+            if ids.dtype != torch.int32 or ids.get_device() != self.device.index or not ids.is_contiguous():
+                ids = ids.to(device=self.device, dtype=torch.int32).contiguous()
+            return ids.reshape(-1), int(ids.numel())
+        a = np.asarray(env_ids.numpy() if isinstance(env_ids, torch.Tensor) else env_ids).reshape(-1)
+        if a.size and a.dtype.kind not in "iu":
+            raise TypeError(f"env ids must be integers, got {a.dtype}")
+        a = a.astype(np.int64)
+        if a.size and (a.min() < -self.E or a.max() >= self.E):
+            raise IndexError(f"env id out of range for {self.E} envs")
+        a = np.where(a < 0, a + self.E, a)
+        if np.unique(a).size != a.size:
+            raise ValueError("duplicate env ids in one call (each listed env is stepped once, in parallel)")
+        return torch.from_numpy(a.astype(np.int32)).to(self.device), int(a.size)
 
     def reset(self, env_ids=None):
         """Environment.reset() for all envs or a subset (QMIX/env_vectorized.py:13-21)."""
         ids, n = self._ids(env_ids)
+        if n == 0:
+            return
         check(lib().mdl_reset(self._h, ptr(ids), n, self._stream()), "mdl_reset")
         self._keep = ids
 
     def clear_tracker(self, env_ids=None):
         ids, n = self._ids(env_ids)
+        if n == 0:
+            return
         check(lib().mdl_tracker_clear(self._h, ptr(ids), n, self._stream()), "mdl_tracker_clear")
         self._keep = ids
+
+    def _check_out(self, out, shape):
+        """The caller's (r_env f64, r_shaped f32, done uint8) buffers: dtype, device, size.
+        The last checked tuple is remembered, so a step loop that reuses its buffers pays
+        for this once."""
+        memo = self._out_ok
+        if memo is not None and len(out) == 3 and all(a is b for a, b in zip(out, memo[0])) \
+                and memo[1] == shape and memo[2] == tuple(t.data_ptr() for t in out):
+            return
+        if len(out) != 3:
+            raise ValueError("out must be (r_env, r_shaped, done)")
+        want = 1
+        for s in shape:
+            want *= s
+        for t, dt, name in zip(out, (torch.float64, torch.float32, torch.uint8), ("r_env", "r_shaped", "done")):
+            if not isinstance(t, torch.Tensor) or t.dtype != dt:
+                raise TypeError(f"out {name} must be a {dt} tensor")
+            if not t.is_cuda or t.get_device() != self.device.index or not t.is_contiguous():
+                raise ValueError(f"out {name} must be contiguous on {self.device}")
+            if t.numel() < want:
+                raise ValueError(f"out {name} holds {t.numel()} entries, needs {want}")
+        self._out_ok = (tuple(out), shape, tuple(t.data_ptr() for t in out))
+
+    def _step_args(self, actions, n, lead=()):
+        if actions.dtype != torch.uint8 or not actions.is_cuda or actions.get_device() != self.device.index \
+                or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=torch.uint8).contiguous()
+        if actions.numel() != n * self.A * (lead[0] if lead else 1) \
+                or (lead and (actions.dim() != 3 or actions.shape[1] != n or actions.shape[2] != self.A)):
+            raise ValueError(f"actions must be [{', '.join(str(x) for x in lead + (n, self.A))}]")
+        return actions
 
     def step(self, actions: torch.Tensor, env_ids=None, auto_reset: bool = True, action_format: str = "int",
              out=None):
@@ -158,19 +225,21 @@ class BatchedEnv:
         actions: uint8 tensor [n, A] on the device -- trainer ints 0..14
         (MAPPO/trainer.py:198-205) or packed codes (action_format="codes").
         Returns (r_env f64 [n], r_shaped f32 [n], done uint8 [n]) views of
-        reusable buffers unless ``out`` is given.
+        reusable buffers unless ``out`` is given (then: float64 / float32 / uint8
+        tensors of >= n entries on the engine's device).
         """
         ids, n = self._ids(env_ids)
-        if actions.dtype != torch.uint8 or actions.device != self.device or not actions.is_contiguous():
-            actions = actions.to(device=self.device, dtype=torch.uint8).contiguous()
-        if actions.numel() != n * self.A:
-            raise ValueError(f"actions must hold {n}x{self.A} entries")
+        actions = self._step_args(actions, n)
         if out is None:
             r, sh, d = self._r[:n], self._sh[:n], self._done[:n]
         else:
+            self._check_out(out, (n,))
             r, sh, d = out
-        check(lib().mdl_step(self._h, ptr(actions), ACTION_FORMATS[action_format], ptr(ids), n, int(bool(auto_reset)),
-                             ptr(r), ptr(sh), ptr(d), self._stream()), "mdl_step")
+        if n == 0:
+            return r, sh, d
+        check(self._fn_step(self._h, actions.data_ptr(), ACTION_FORMATS[action_format], ptr(ids), n,
+                            int(bool(auto_reset)), r.data_ptr(), sh.data_ptr(), d.data_ptr(),
+                            _raw_stream(self.device.index)), "mdl_step")
         self._keep = (ids, actions)
         return r, sh, d
 
@@ -182,17 +251,19 @@ class BatchedEnv:
         done uint8 [K, n]), identical to K ``step`` calls with actions[k].
         """
         ids, n = self._ids(env_ids)
-        if actions.dtype != torch.uint8 or actions.device != self.device or not actions.is_contiguous():
-            actions = actions.to(device=self.device, dtype=torch.uint8).contiguous()
-        if actions.dim() != 3 or actions.shape[1] != n or actions.shape[2] != self.A:
+        if actions.dim() != 3:
             raise ValueError(f"actions must be [K, {n}, {self.A}]")
         K = actions.shape[0]
+        actions = self._step_args(actions, n, (K,))
         if out is None:
             r = torch.empty((K, n), dtype=torch.float64, device=self.device)
             sh = torch.empty((K, n), dtype=torch.float32, device=self.device)
             d = torch.empty((K, n), dtype=torch.uint8, device=self.device)
         else:
+            self._check_out(out, (K, n))
             r, sh, d = out
+        if n == 0 or K == 0:
+            return r, sh, d
         check(lib().mdl_step_fused(self._h, ptr(actions), ACTION_FORMATS[action_format], ptr(ids), n, K,
                                    int(bool(auto_reset)), ptr(r), ptr(sh), ptr(d), self._stream()), "mdl_step_fused")
         self._keep = (ids, actions)
@@ -208,15 +279,46 @@ class BatchedEnv:
                     critic_map=torch.empty((n, 4, H, W), **f),
                     critic_vec=torch.empty((n, self.critic_vec_dim), **f))
 
+    def _obs_range(self, env_begin, n):
+        """Checked env range of one observation call -> (n, grid of its map shape)."""
+        env_begin = int(env_begin)
+        n = self.E - env_begin if n is None else int(n)
+        if env_begin < 0 or n < 0 or env_begin + n > self.E:
+            raise IndexError(f"env range [{env_begin}, {env_begin + n}) outside [0, {self.E})")
+        if n == 0:
+            return n, self.grids[0]
+        if self._shape_run_end[env_begin] < env_begin + n:
+            raise ValueError(f"envs [{env_begin}, {env_begin + n}) mix map shapes: build observations per "
+                             f"same-shape group (this one ends at env {int(self._shape_run_end[env_begin])})")
+        return n, self.grids[int(self.env_map[env_begin])]
+
+    @staticmethod
+    def _check_obs_out(t, name, shape):
+        want = 1
+        for s in shape:
+            want *= s
+        if not isinstance(t, torch.Tensor) or t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+            raise TypeError(f"{name} must be a contiguous float32 device tensor")
+        if t.numel() < want:
+            raise ValueError(f"{name} holds {t.numel()} floats, needs {want} {tuple(shape)}")
+
     def build_obs(self, env_begin: int = 0, n: int | None = None, out: dict | None = None,
                   which=("actor_map", "actor_vec", "critic_map", "critic_vec")):
         """convert_observation / generate_vector_features / convert_global_state
-        for every agent of envs [env_begin, env_begin+n) (one map shape)."""
-        n = self.E - env_begin if n is None else n
-        g = self.grids[int(self.env_map[env_begin])] if n else self.grids[0]
+        for every agent of envs [env_begin, env_begin+n) (one map shape: raises
+        on a range that mixes map shapes)."""
+        n, g = self._obs_range(env_begin, n)
+        H, W = g.shape
         if out is None:
-            out = self.obs_buffers(n, g.shape[0], g.shape[1])
+            out = self.obs_buffers(n, H, W)
         p = {k: (out[k] if k in which else None) for k in ("actor_map", "actor_vec", "critic_map", "critic_vec")}
+        shapes = dict(actor_map=(n, self.A, 6, H, W), actor_vec=(n, self.A, self.actor_vec_dim),
+                      critic_map=(n, 4, H, W), critic_vec=(n, self.critic_vec_dim))
+        for k, t in p.items():
+            if t is not None:
+                self._check_obs_out(t, k, shapes[k])
+        if n == 0:
+            return out
         check(lib().mdl_build_obs(self._h, env_begin, n, ptr(p["actor_map"]), ptr(p["actor_vec"]),
                                   ptr(p["critic_map"]), ptr(p["critic_vec"]), self._stream()), "mdl_build_obs")
         return out
@@ -228,8 +330,7 @@ class BatchedEnv:
         convert_global_state_to_tensor (qmix/networks.py:350-468) for envs [env_begin, env_begin+n).
         state_shape (7, h, w) defaults to the map's (7, H, W) as the qmix trainer uses; build the
         engine with tracker="fresh" for the IDQ / qmix trainers' per-episode trackers."""
-        n = self.E - env_begin if n is None else n
-        g = self.grids[int(self.env_map[env_begin])] if n else self.grids[0]
+        n, g = self._obs_range(env_begin, n)
         H, W = g.shape
         oh, ow = (H, W) if state_shape is None else (int(state_shape[1]), int(state_shape[2]))
         if out is None:
@@ -239,6 +340,12 @@ class BatchedEnv:
                 out["idq_obs"] = torch.empty((n, self.A, 6, H, W), **f)
             if "qmix_state" in which:
                 out["qmix_state"] = torch.empty((n, 7, oh, ow), **f)
+        if out.get("idq_obs") is not None:
+            self._check_obs_out(out["idq_obs"], "idq_obs", (n, self.A, 6, H, W))
+        if out.get("qmix_state") is not None:
+            self._check_obs_out(out["qmix_state"], "qmix_state", (n, 7, oh, ow))
+        if n == 0:
+            return out
         check(lib().mdl_build_obs_alt(self._h, env_begin, n, ptr(out.get("idq_obs")), ptr(out.get("qmix_state")),
                                       oh, ow, self._stream()), "mdl_build_obs_alt")
         return out
@@ -247,6 +354,8 @@ class BatchedEnv:
     def greedy_init(self, env_ids=None):
         """``GreedyAgents()`` + ``init_agents(state)`` for the listed envs (right after their reset)."""
         ids, n = self._ids(env_ids)
+        if n == 0 and env_ids is not None:
+            return
         check(lib().mdl_greedy_init(self._h, ptr(ids), n, self._stream()), "mdl_greedy_init")
         self._keep_g = ids
 
@@ -255,6 +364,10 @@ class BatchedEnv:
         ids, n = self._ids(env_ids)
         if out is None:
             out = torch.empty((n, self.A), dtype=torch.uint8, device=self.device)
+        elif out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or out.numel() < n * self.A:
+            raise ValueError(f"out must be a contiguous uint8 device tensor of >= {n}x{self.A} entries")
+        if n == 0:
+            return out
         check(lib().mdl_greedy_actions(self._h, ptr(ids), n, ptr(out), self._stream()), "mdl_greedy_actions")
         self._keep_g = ids
         return out

@@ -107,7 +107,7 @@ class MappoRollout:
         self.next_obs = env.obs_buffers(E, H, W)
         self._r_env = torch.zeros(E, dtype=torch.float64, device=dev)
         self._graph = None          # hipGraph of one whole rollout (collect(graph=True))
-        self._graph_key = None
+        self._graph_key = None      # (actor, critic, parameter addresses) the graph was captured with
         self._graph_out = None
         self._off_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # sampler offset base (uint64 bits)
 
@@ -125,8 +125,13 @@ class MappoRollout:
         static buffers: consume them before the next collect."""
         if not graph:
             return self._run(actor, critic, False)
-        key = (id(actor), id(critic))
-        if self._graph is not None and self._graph_key == key:
+        # the graph reads the modules' parameters in place: replay only for the very same modules
+        # (strong references, compared by identity) whose parameters still live at the captured
+        # addresses (load_state_dict copies in place; rebinding ``param.data`` does not)
+        ptrs = tuple(q.data_ptr() for m in (actor, critic) if hasattr(m, "parameters") for q in m.parameters())
+        key = (actor, critic, ptrs)
+        k0 = self._graph_key
+        if self._graph is not None and k0[0] is actor and k0[1] is critic and k0[2] == ptrs:
             self._graph.replay()
             self.offset += self.T
             return self._graph_out

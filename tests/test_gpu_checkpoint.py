@@ -73,3 +73,57 @@ def test_checkpoint_refuses_other_configuration():
     bad[:8] = 0
     with pytest.raises(mg.MdlError):
         mg.BatchedEnv(grid("map1.txt"), 16, 5, 50, 100, seed=1).load_state(bad)
+
+
+def test_checkpoint_refuses_other_constants_and_obs_dims():
+    """Reward constants, shaping constants and observation dims are part of the
+    checkpoint's configuration fingerprint (a snapshot used to load into
+    an engine that would then compute other rewards / features)."""
+    mg = _mg()
+    base = dict(seed=1)
+    a = mg.BatchedEnv(grid("map1.txt"), 16, 5, 50, 100, **base)
+    a.reset()
+    blob = a.save_state()
+    mg.BatchedEnv(grid("map1.txt"), 16, 5, 50, 100, **base).load_state(blob)   # same configuration: loads
+    for kw in (dict(move_cost=-0.02), dict(delivery_reward=5.0), dict(delay_reward=2.0), dict(shaping="qmix"),
+               dict(max_packages_obs=100), dict(max_other_robots=10), dict(max_robots_state=10),
+               dict(max_packages_state=20), dict(obs_max_time_steps=50)):
+        other = mg.BatchedEnv(grid("map1.txt"), 16, 5, 50, 100, **base, **kw)
+        with pytest.raises(mg.MdlError, match="constants or observation"):
+            other.load_state(blob)
+
+
+def test_checkpoint_carries_greedy_agents():
+    """The greedy agents' records travel with the checkpoint: a restored engine's
+    greedy_actions continue the saved run action for action.  A checkpoint without
+    them makes an engine's own greedy records stale until greedy_init."""
+    mg = _mg()
+    g = grid("map1.txt")
+    E, A, P, T = 64, 5, 40, 60
+    a = mg.BatchedEnv(g, E, A, P, T, seed=9, tracker="fresh")
+    a.reset()
+    a.greedy_init()
+    for _ in range(20):
+        a.step(a.greedy_actions(), auto_reset=False, action_format="codes")
+    blob = a.save_state()
+    want = []
+    for _ in range(30):
+        act = a.greedy_actions()
+        want.append(act.cpu())
+        a.step(act, auto_reset=False, action_format="codes")
+    b = mg.BatchedEnv(g, E, A, P, T, seed=9, tracker="fresh")
+    b.load_state(blob)
+    for k in range(30):
+        act = b.greedy_actions()
+        assert torch.equal(act.cpu(), want[k]), k
+        b.step(act, auto_reset=False, action_format="codes")
+    # a checkpoint taken before greedy_init has no greedy section
+    c = mg.BatchedEnv(g, E, A, P, T, seed=9, tracker="fresh")
+    c.reset()
+    plain = c.save_state()
+    assert plain.nbytes < blob.nbytes
+    b.load_state(plain)
+    with pytest.raises(mg.MdlError, match="greedy_init"):
+        b.greedy_actions()
+    b.greedy_init()
+    b.greedy_actions()

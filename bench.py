@@ -177,6 +177,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    def stop_clock(t_start):
+        """End of a timed region: this rank's GPU work drained, then its clock read, then
+        the barrier -- the collective's own latency stays outside the measured time (the
+        start is aligned by the opening barrier; the MAX over ranks below covers skew)."""
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t_start
+        if dist is not None:
+            dist.barrier()
+        return dt
+
     # ---- timed region: K steps replayed from graphs ----
     barrier()
     t0 = time.perf_counter()
@@ -189,8 +199,7 @@ def main():
         for k in range(K):
             one(k)
     ev1.record()
-    barrier()
-    wall = time.perf_counter() - t0
+    wall = stop_clock(t0)
     gpu_ms = ev0.elapsed_time(ev1)
 
     # ---- eager throughput (same kernels, one ctypes launch per step) ----
@@ -200,8 +209,7 @@ def main():
         t1 = time.perf_counter()
         for k in range(K):
             one(k)
-        barrier()
-        wall_eager = time.perf_counter() - t1
+        wall_eager = stop_clock(t1)
 
     # ---- bench mode: fused_k steps per launch, each env's
     # state in registers between steps; same action stream; not the API path ----
@@ -217,8 +225,7 @@ def main():
         t2 = time.perf_counter()
         for _ in range(nf):
             env.step_fused(facts, out=(fr, fsh, fdn))
-        barrier()
-        wall_f = time.perf_counter() - t2
+        wall_f = stop_clock(t2)
 
     # ---- per-launch kernel duration: HIP events on the launch stream around the
     # timed region (back-to-back launches, so this includes the ~1 us dispatch
@@ -269,6 +276,7 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
+            "graph_upload_replay_steps": 0 if graph is None else G,
             "ms_per_step": wall / K * 1e3,
             "higher_is_better": True,
             "scaling": "strong" if args.total_envs > 0 else "weak",

@@ -68,6 +68,10 @@ class BatchedEnv:
         if not torch.cuda.is_available():
             raise RuntimeError("marl_gpu.BatchedEnv needs a ROCm GPU (no CPU fallback)")
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError(f"marl_gpu.BatchedEnv runs on a GPU device, not {self.device}")
+        if self.device.index is None:   # "cuda" -> the current device, explicitly
+            self.device = torch.device("cuda", torch.cuda.current_device())
         if isinstance(maps, (str, np.ndarray)) or (isinstance(maps, list) and maps and isinstance(maps[0], list)
                                                   and maps[0] and isinstance(maps[0][0], (int, np.integer))):
             maps = [maps]
@@ -121,6 +125,8 @@ class BatchedEnv:
         self._done = torch.zeros(self.E, dtype=torch.uint8, device=self.device)
         self._fn_step = lib().mdl_step
         self._out_ok = None
+        self._dev = self.device.index
+        self._full_out = (self._r, self._sh, self._done)
         # end (exclusive) of each env's run of consecutive envs with the same map shape:
         # an observation range must lie inside one run (its tensors have one H x W)
         hw_env = np.array([self.grids[m].shape for m in self.env_map], np.int64).reshape(self.E, 2)
@@ -189,12 +195,8 @@ class BatchedEnv:
 
     def _check_out(self, out, shape):
         """The caller's (r_env f64, r_shaped f32, done uint8) buffers: dtype, device, size.
-        The last checked tuple is remembered, so a step loop that reuses its buffers pays
-        for this once."""
-        memo = self._out_ok
-        if memo is not None and len(out) == 3 and all(a is b for a, b in zip(out, memo[0])) \
-                and memo[1] == shape and memo[2] == tuple(t.data_ptr() for t in out):
-            return
+        The last checked buffers are remembered (objects, shape, addresses), so a step loop
+        that reuses its buffers pays for the full check once."""
         if len(out) != 3:
             raise ValueError("out must be (r_env, r_shaped, done)")
         want = 1
@@ -207,7 +209,16 @@ class BatchedEnv:
                 raise ValueError(f"out {name} must be contiguous on {self.device}")
             if t.numel() < want:
                 raise ValueError(f"out {name} holds {t.numel()} entries, needs {want}")
-        self._out_ok = (tuple(out), shape, tuple(t.data_ptr() for t in out))
+        self._out_ok = (out[0], out[1], out[2], shape, (out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr()))
+
+    def _out_ptrs(self, out, shape):
+        """Addresses of checked output buffers (the full check only for new buffers)."""
+        r, sh, d = out
+        ptrs = (r.data_ptr(), sh.data_ptr(), d.data_ptr())
+        m = self._out_ok
+        if m is None or r is not m[0] or sh is not m[1] or d is not m[2] or m[3] != shape or m[4] != ptrs:
+            self._check_out(out, shape)
+        return ptrs
 
     def _step_args(self, actions, n, lead=()):
         if actions.dtype != torch.uint8 or not actions.is_cuda or actions.get_device() != self.device.index \
@@ -228,20 +239,25 @@ class BatchedEnv:
         reusable buffers unless ``out`` is given (then: float64 / float32 / uint8
         tensors of >= n entries on the engine's device).
         """
-        ids, n = self._ids(env_ids)
-        actions = self._step_args(actions, n)
-        if out is None:
-            r, sh, d = self._r[:n], self._sh[:n], self._done[:n]
+        if env_ids is None:
+            ids, n = None, self.E
         else:
-            self._check_out(out, (n,))
-            r, sh, d = out
+            ids, n = self._ids(env_ids)
+        if actions.dtype is not torch.uint8 or not actions.is_cuda or not actions.is_contiguous() \
+                or actions.get_device() != self._dev or actions.numel() != n * self.A:
+            actions = self._step_args(actions, n)
+        if out is None:
+            out = self._full_out if n == self.E else (self._r[:n], self._sh[:n], self._done[:n])
+            ptrs = (out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr())
+        else:
+            ptrs = self._out_ptrs(out, (n,))
         if n == 0:
-            return r, sh, d
-        check(self._fn_step(self._h, actions.data_ptr(), ACTION_FORMATS[action_format], ptr(ids), n,
-                            int(bool(auto_reset)), r.data_ptr(), sh.data_ptr(), d.data_ptr(),
-                            _raw_stream(self.device.index)), "mdl_step")
+            return out
+        check(self._fn_step(self._h, actions.data_ptr(), ACTION_FORMATS[action_format],
+                            None if ids is None else ids.data_ptr(), n, 1 if auto_reset else 0,
+                            ptrs[0], ptrs[1], ptrs[2], _raw_stream(self._dev)), "mdl_step")
         self._keep = (ids, actions)
-        return r, sh, d
+        return out[0], out[1], out[2]
 
     def step_fused(self, actions: torch.Tensor, env_ids=None, auto_reset: bool = True, action_format: str = "int",
                    out=None):
@@ -260,7 +276,7 @@ class BatchedEnv:
             sh = torch.empty((K, n), dtype=torch.float32, device=self.device)
             d = torch.empty((K, n), dtype=torch.uint8, device=self.device)
         else:
-            self._check_out(out, (K, n))
+            self._out_ptrs(out, (K, n))
             r, sh, d = out
         if n == 0 or K == 0:
             return r, sh, d

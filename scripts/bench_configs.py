@@ -40,6 +40,30 @@ def timed(fn, n):
     return s.elapsed_time(e) / n * 1e3  # us per call
 
 
+def graph_timed(fn, G, reps):
+    """us per step of G captured calls fn(0..G-1) replayed `reps` times (after one untimed
+    replay): the kernels without the host launch path."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        fn(0)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            for k in range(G):
+                fn(k)
+    torch.cuda.synchronize()
+    g.replay()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / (G * reps) * 1e3
+
+
 def run(cfg, steps, warmup):
     import marl_gpu
     from marl_gpu.maps import grid_array, load_map, map_path
@@ -74,8 +98,13 @@ def run(cfg, steps, warmup):
         bufs = env.obs_buffers()
     for k in range(warmup):
         env.step(acts[k % G])
-    step_us = timed(lambda k: env.step(acts[k % G]), steps)
-    out["step_us"] = step_us
+    step_eager_us = timed(lambda k: env.step(acts[k % G]), steps)
+    r = torch.zeros(E, dtype=torch.float64, device=dev)
+    sh = torch.zeros(E, dtype=torch.float32, device=dev)
+    dn = torch.zeros(E, dtype=torch.uint8, device=dev)
+    step_us = graph_timed(lambda k: env.step(acts[k % G], out=(r, sh, dn)), G, max(1, steps // G))
+    out["step_us"] = step_us          # hipGraph-replayed steps (the kernel path)
+    out["step_eager_us"] = step_eager_us
     out["agent_steps_per_s_step_only"] = E * A / (step_us * 1e-6)
     step_bytes = (9 * A + 10 * P + 41) * E
     out["step_roofline"] = {"achieved_GBs": step_bytes / (step_us * 1e-6) / 1e9, "frac": step_bytes / (step_us * 1e-6) / 1e9 / HBM}

@@ -90,6 +90,17 @@ int mdl_tracker_clear(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* s
 int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
              int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
 
+/* mdl_step for all E envs followed by mdl_build_obs(eng, 0, E, ...) of the new state --
+ * the trainer's per-step sequence (MAPPO/trainer.py:229-286: env.step, reset on done,
+ * tracker update, then convert_observation x A, generate_vector_features x A and
+ * convert_global_state of the next state).  Same outputs as the two calls (bit-exact);
+ * for A <= 8, P <= 64 they run as ONE kernel that builds the observations from the
+ * state the step leaves in registers (no second launch, no state reload), otherwise
+ * as the two launches.  The E envs must share one map shape; any output may be NULL. */
+int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, int32_t auto_reset, double* r_env,
+                 float* r_shaped, uint8_t* done, float* actor_map, float* actor_vec, float* critic_map,
+                 float* critic_vec, void* stream);
+
 /* Bench mode: k_steps consecutive mdl_step calls fused
  * into one launch, each env's state held in registers between steps.  Same
  * results as k_steps mdl_step calls with actions[k] (bit-exact); actions are

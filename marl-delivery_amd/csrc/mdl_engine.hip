@@ -466,6 +466,34 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
     return 0;
 }
 
+int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, int32_t auto_reset, double* r_env,
+                 float* r_shaped, uint8_t* done, float* actor_map, float* actor_vec, float* critic_map,
+                 float* critic_vec, void* stream) {
+    if (!eng || !actions) return fail("mdl_step_obs: null argument");
+    if (!eng->seeded) return fail("mdl_step_obs: engine not seeded (call mdl_seed first)");
+    if (action_format != MDL_ACTION_TRAINER_INT && action_format != MDL_ACTION_CODES)
+        return fail("mdl_step_obs: unknown action_format %d", action_format);
+    const int E = eng->p.E;
+    if (eng->shape_run_end[0] < E)
+        return fail("mdl_step_obs: the envs mix map shapes (same-shape run ends at %d); use mdl_step + mdl_build_obs "
+                    "per group", eng->shape_run_end[0]);
+    DeviceGuard dg(eng->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (eng->p.obs_small && eng->p.A <= 8 && eng->p.P <= 64) {
+        const size_t lds = std::max(eng->lds_step, eng->lds_obs);   // one slice: reset scratch, then the planes
+        const int wpb = waves_per_block(lds);
+        if (wpb >= 1) {
+            HIPCHK(mdl::launch_step_obs(eng->p, actions, action_format, E, auto_reset, r_env, r_shaped, done,
+                                        actor_map, actor_vec, critic_map, critic_vec, wpb, lds, s));
+            return 0;
+        }
+    }
+    HIPCHK(mdl::launch_step(eng->p, actions, action_format, nullptr, E, auto_reset, r_env, r_shaped, done,
+                            eng->wpb_step, eng->lds_step, s));
+    HIPCHK(mdl::launch_obs(eng->p, 0, E, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs, eng->lds_obs, s));
+    return 0;
+}
+
 int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
                    int32_t k_steps, int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream) {
     if (!eng || !actions) return fail("mdl_step_fused: null argument");

@@ -317,14 +317,25 @@ struct StepKarg {
 };
 constexpr uint32_t NW_IDS = 1u << 29, NW_MAP = 1u << 30;
 
-template <bool STALE, int NCH, bool FUSED, int AU>
-__global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict__ rob_pre,
-                                                      const uint64_t* __restrict__ pkg_pre,
-                                                      const uint16_t* __restrict__ pst_pre,
-                                                      const u32x4* __restrict__ es_pre,
-                                                      const uint64_t* __restrict__ trk_pre,
-                                                      const uint8_t* __restrict__ act_pre, uint32_t ap,
-                                                      uint32_t nw, StepArgs args) {
+// The fused step + observation launch's extra arguments (after StepArgs in its kernarg
+// segment, so the StepKarg prefix -- preloaded SGPRs, the late kernarg batch -- is the same).
+struct ObsArgs {
+    float* amap;
+    float* avec;
+    float* cmap;
+    float* cvec;
+};
+
+// The step kernel's body.  OBS (NCH = 1, A <= 8, k_obs_small's configurations): after the
+// write-back the wave builds the env's observations of the new state from the registers the
+// step leaves (robots on lanes < A, package j on lane j), as MAPPO/trainer.py:229-286 does
+// after every env.step -- one launch and no state reload instead of k_step + k_obs_small.
+template <bool STALE, int NCH, bool FUSED, int AU, bool OBS>
+__device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, const uint64_t* __restrict__ pkg_pre,
+                                          const uint16_t* __restrict__ pst_pre, const u32x4* __restrict__ es_pre,
+                                          const uint64_t* __restrict__ trk_pre, const uint8_t* __restrict__ act_pre,
+                                          uint32_t ap, uint32_t nw, const StepArgs& args, const ObsArgs& oa) {
+    static_assert(!OBS || (NCH == 1 && !FUSED && AU > 0 && AU <= 8), "fused observations: P <= 64, A <= 8");
     extern __shared__ __align__(16) unsigned char smem[];
     const DevParams& p = args.p;
     // (the other scalar arguments are read only after the state loads are issued: read
@@ -845,6 +856,33 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
     if (lane == 0)
         for (int k = 0; k < 16; k++) g_stamps[(size_t)w * 16 + k] = stamp_[k];
 #endif
+    if constexpr (OBS)   // full batch only (no env_ids): output row w = env e
+        obs_small_emit<STALE>(p, w, mi, act ? rob_pack(cell, carry, vmask) : 0u, pk[0], ps[0], STALE ? td[0] : 0ull,
+                              t_cur, oa.amap, oa.avec, oa.cmap, oa.cvec, smem + (size_t)wave * lds_stride);
+}
+
+template <bool STALE, int NCH, bool FUSED, int AU>
+__global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict__ rob_pre,
+                                                      const uint64_t* __restrict__ pkg_pre,
+                                                      const uint16_t* __restrict__ pst_pre,
+                                                      const u32x4* __restrict__ es_pre,
+                                                      const uint64_t* __restrict__ trk_pre,
+                                                      const uint8_t* __restrict__ act_pre, uint32_t ap,
+                                                      uint32_t nw, StepArgs args) {
+    step_body<STALE, NCH, FUSED, AU, false>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre, act_pre, ap, nw, args,
+                                            ObsArgs{});
+}
+
+// mdl_step_obs: k_step + k_obs_small in one launch (full batch, NCH = 1, A <= 8)
+template <bool STALE, int AU>
+__global__ __launch_bounds__(256) void k_step_obs(const uint32_t* __restrict__ rob_pre,
+                                                  const uint64_t* __restrict__ pkg_pre,
+                                                  const uint16_t* __restrict__ pst_pre,
+                                                  const u32x4* __restrict__ es_pre,
+                                                  const uint64_t* __restrict__ trk_pre,
+                                                  const uint8_t* __restrict__ act_pre, uint32_t ap, uint32_t nw,
+                                                  StepArgs args, ObsArgs oa) {
+    step_body<STALE, 1, false, AU, true>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre, act_pre, ap, nw, args, oa);
 }
 
 // ------------------------------------------------------------- observations
@@ -1335,6 +1373,41 @@ hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, cons
                        double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
     if (p.stale) launch_step_s<true, false>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, 1, s);
     else launch_step_s<false, false>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, 1, s);
+    return hipGetLastError();
+}
+
+// k_step_obs (mdl_step_obs): full batch, NCH = 1, A <= 8, the small observation builder;
+// lds = the per-wave slice (max of the step's reset scratch and the builder's planes)
+hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
+                           float* sh, uint8_t* done, float* amap, float* avec, float* cmap, float* cvec, int wpb,
+                           size_t lds, hipStream_t s) {
+    if (nch_for(p.P) != 1 || p.A > 8 || !p.obs_small) return hipErrorInvalidValue;
+    StepArgs a;
+    a.p = p;
+    a.actions = actions;
+    a.env_ids = nullptr;
+    a.r_out = r;
+    a.sh_out = sh;
+    a.done_out = done;
+    a.fmt = fmt;
+    a.n = n;
+    a.auto_reset = auto_reset;
+    a.wpb = wpb;
+    a.lds_stride = (int)lds;
+    a.K = 1;
+    const ObsArgs o{amap, avec, cmap, cvec};
+    const dim3 grid(blocks_for(n, wpb)), block(256);
+    const uint32_t ap = (uint32_t)p.A | ((uint32_t)p.P << 16);
+    const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
+#define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a, o
+    if (p.stale) {
+        if (p.A == 5) hipLaunchKernelGGL((k_step_obs<true, 5>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+        else hipLaunchKernelGGL((k_step_obs<true, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    } else {
+        if (p.A == 5) hipLaunchKernelGGL((k_step_obs<false, 5>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+        else hipLaunchKernelGGL((k_step_obs<false, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    }
+#undef MDL_STEP_ARGS
     return hipGetLastError();
 }
 

@@ -19,6 +19,9 @@ hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, cons
 hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int K,
                              int auto_reset, double* r, float* sh, uint8_t* done, int wpb, size_t lds,
                              hipStream_t s);
+hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
+                           float* sh, uint8_t* done, float* amap, float* avec, float* cmap, float* cvec, int wpb,
+                           size_t lds, hipStream_t s);
 hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
                       int wpb, size_t lds, hipStream_t s);
 hipError_t launch_views_features(const DevParams& p, const int32_t* views, const int64_t* offs, int n,

@@ -195,18 +195,18 @@ __host__ __device__ inline bool obs_small_ok(int A, int P, int key7_dsh, int max
     return A >= 1 && A <= 8 && P >= 1 && P <= WAVE && key7_dsh > 0 && obs_small_lds(A, maxHW) <= 16384;
 }
 
+// The builder's body for env e (output row w) from its state words as the lanes hold
+// them: lane a < A the robot word, lane j < P package j's table entry, state word and
+// (stale mode) tracker data, t the env clock.  k_obs_small loads them; the fused
+// step + observation kernel (k_step<..., OBS = true>) passes the step's registers.
+// `smem_wave` is this wave's LDS slice (obs_small_lds bytes).
 template <bool STALE>
-__global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, int n, float* __restrict__ amap,
-                                                   float* __restrict__ avec, float* __restrict__ cmap,
-                                                   float* __restrict__ cvec, int wpb, int lds_stride) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = wave_id();
+__device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi, uint32_t rv, uint64_t pkd,
+                                               uint32_t f, uint64_t tdd, int t, float* __restrict__ amap,
+                                               float* __restrict__ avec, float* __restrict__ cmap,
+                                               float* __restrict__ cvec, unsigned char* smem_wave) {
     const int lane = lane_id();
-    const int w = blockIdx.x * wpb + wave;
-    if (wave >= wpb || w >= n) return;
-    const int e = env_begin + w;
     const int A = p.A, P = p.P;
-    const int mi = p.env_map ? p.env_map[e] : 0;
     const MapDesc md = p.maps[mi];
     const int H = md.H, W = md.W, HW = H * W, NW = (HW + 31) / 32;
     const int T = p.obsT, MO = p.MO, MP = p.MP, MR = p.MR, MPs = p.MPs;
@@ -217,27 +217,16 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
     const uint16_t* rank = p.rank + md.rank_off;
     const int rW = 2 * W - 1, rOff = (H - 1) * rW + (W - 1);   // rank[(dr+H-1)*(2W-1) + dc+W-1]
 
-    uint32_t* bits = (uint32_t*)(smem + (size_t)wave * lds_stride);   // [5][NW] + guard, critic planes first
-    uint32_t* planes = bits + 5 * NW + 1;                             // flat image of the 6A actor planes
-    uint32_t* cplanes = planes + 6 * A * NW;                          // flat image of the 4 critic planes
-    int* scar = (int*)(cplanes + 4 * NW);                             // [64] carrier robot of a slot
-    int* invc = scar + 64;                                            // [64] critic row -> slot
-    uint8_t* o2j = (uint8_t*)(invc + 64);                             // [128] 7-bit order -> slot
-    uint8_t* invp = o2j + 128;                                        // [8][64] (agent, rank) -> slot
-    int* aidx = (int*)(invp + 512);                                   // [8][2] agent's cell, carried target
+    uint32_t* bits = (uint32_t*)smem_wave;                       // [5][NW] + guard, critic planes first
+    uint32_t* planes = bits + 5 * NW + 1;                         // flat image of the 6A actor planes
+    uint32_t* cplanes = planes + 6 * A * NW;                      // flat image of the 4 critic planes
+    int* scar = (int*)(cplanes + 4 * NW);                         // [64] carrier robot of a slot
+    int* invc = scar + 64;                                        // [64] critic row -> slot
+    uint8_t* o2j = (uint8_t*)(invc + 64);                         // [128] 7-bit order -> slot
+    uint8_t* invp = o2j + 128;                                    // [8][64] (agent, rank) -> slot
+    int* aidx = (int*)(invp + 512);                               // [8][2] agent's cell, carried target
 
-    // ---- loads: robots, packages (+ tracker data), clock ----
     const bool rl = lane < A, pl = lane < P;
-    const uint32_t rv = rl ? p.rob[(size_t)e * A + lane] : 0u;
-    uint64_t pkd = 0, tdd = 0;
-    uint32_t f = 0;
-    if (pl) {
-        const size_t g = (size_t)e * P + lane;
-        pkd = p.pkg[g];
-        f = p.pstate[g];
-        if (STALE) tdd = p.trk[g];
-    }
-    const int t = p.es[e].t;
     if (lane == 0) bits[5 * NW] = 0;   // guard word read (and masked off) by bits_at
     for (int k = lane; k < NW; k += WAVE) {
         bits[BS_GRID * NW + k] = p.gridbits[md.bits_off + k];
@@ -514,6 +503,32 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
         }
         if (lane == 0) cv[Dg - 1] = qdiv_r(t, yT);
     }
+}
+
+template <bool STALE>
+__global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, int n, float* __restrict__ amap,
+                                                   float* __restrict__ avec, float* __restrict__ cmap,
+                                                   float* __restrict__ cvec, int wpb, int lds_stride) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int wave = wave_id();
+    const int lane = lane_id();
+    const int w = blockIdx.x * wpb + wave;
+    if (wave >= wpb || w >= n) return;
+    const int e = env_begin + w;
+    const int A = p.A, P = p.P;
+    const int mi = p.env_map ? p.env_map[e] : 0;
+    // ---- loads: robots, packages (+ tracker data), clock ----
+    const uint32_t rv = lane < A ? p.rob[(size_t)e * A + lane] : 0u;
+    uint64_t pkd = 0, tdd = 0;
+    uint32_t f = 0;
+    if (lane < P) {
+        const size_t g = (size_t)e * P + lane;
+        pkd = p.pkg[g];
+        f = p.pstate[g];
+        if (STALE) tdd = p.trk[g];
+    }
+    const int t = p.es[e].t;
+    obs_small_emit<STALE>(p, w, mi, rv, pkd, f, tdd, t, amap, avec, cmap, cvec, smem + (size_t)wave * lds_stride);
 }
 
 }  // namespace mdl

@@ -54,6 +54,7 @@ SIGNATURES = {
     "mdl_reset": (C.c_int, [_vp, _vp, _i32, _vp]),
     "mdl_tracker_clear": (C.c_int, [_vp, _vp, _i32, _vp]),
     "mdl_step": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "mdl_step_obs": (C.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mdl_step_fused": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mdl_build_obs": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mdl_build_obs_alt": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp]),
@@ -95,6 +96,8 @@ def lib():
                               "(or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if "MDL_LIB_PATH" in os.environ and not hasattr(L, name):
+                continue   # an older profiling build (same-box A/B): entry points it lacks stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -259,6 +259,42 @@ class BatchedEnv:
         self._keep = (ids, actions)
         return out[0], out[1], out[2]
 
+    def step_obs(self, actions: torch.Tensor, auto_reset: bool = True, action_format: str = "int", out=None,
+                 obs_out: dict | None = None, which=("actor_map", "actor_vec", "critic_map", "critic_vec")):
+        """``step`` over all envs, then ``build_obs`` of the new state (the trainer's per-step
+        sequence, MAPPO/trainer.py:229-286), as one launch when A <= 8 and P <= 64: the
+        kernel builds the observations from the state the step leaves in registers.
+        Bit-identical to ``step(...)`` followed by ``build_obs()``.  The envs must share one
+        map shape.  Returns (r_env, r_shaped, done, obs dict)."""
+        n = self.E
+        if actions.dtype is not torch.uint8 or not actions.is_cuda or not actions.is_contiguous() \
+                or actions.get_device() != self._dev or actions.numel() != n * self.A:
+            actions = self._step_args(actions, n)
+        if out is None:
+            out = self._full_out
+            ptrs = (out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr())
+        else:
+            ptrs = self._out_ptrs(out, (n,))
+        if self._shape_run_end[0] < n:
+            raise ValueError("step_obs: the envs mix map shapes; use step() and build_obs() per same-shape group")
+        H, W = self.grids[int(self.env_map[0])].shape
+        if obs_out is None:
+            obs_out = self._obs_cache if getattr(self, "_obs_cache", None) is not None else self.obs_buffers(n, H, W)
+            self._obs_cache = obs_out
+        shapes = dict(actor_map=(n, self.A, 6, H, W), actor_vec=(n, self.A, self.actor_vec_dim),
+                      critic_map=(n, 4, H, W), critic_vec=(n, self.critic_vec_dim))
+        op = {}
+        for k in ("actor_map", "actor_vec", "critic_map", "critic_vec"):
+            t = obs_out.get(k) if k in which else None
+            if t is not None:
+                self._check_obs_out(t, k, shapes[k])
+            op[k] = None if t is None else t.data_ptr()
+        check(lib().mdl_step_obs(self._h, actions.data_ptr(), ACTION_FORMATS[action_format], 1 if auto_reset else 0,
+                                 ptrs[0], ptrs[1], ptrs[2], op["actor_map"], op["actor_vec"], op["critic_map"],
+                                 op["critic_vec"], _raw_stream(self._dev)), "mdl_step_obs")
+        self._keep = (None, actions)
+        return out[0], out[1], out[2], obs_out
+
     def step_fused(self, actions: torch.Tensor, env_ids=None, auto_reset: bool = True, action_format: str = "int",
                    out=None):
         """Bench mode: K consecutive steps in one launch.

@@ -91,6 +91,8 @@ class MappoRollout:
         self.offset = 0
         self.gamma, self.gae_lambda = gamma, gae_lambda
         E, A = env.E, env.A
+        if env._shape_run_end[0] < E:   # the buffers hold one [H, W]; a mixed-shape batch needs one rollout per group
+            raise ValueError("MappoRollout: the engine's envs mix map shapes (build one engine per map shape)")
         H, W = env.grids[int(env.env_map[0])].shape
         dev = env.device
         f = dict(dtype=torch.float32, device=dev)
@@ -169,9 +171,10 @@ class MappoRollout:
                 sample_actions(logits, self.seed, self.offset, out=acts_lp)
             self.offset += 1
             self.mb_values[step] = critic(self.mb_global_states[step], self.mb_global_vector[step]).reshape(E)
-            env.step(self.mb_actions[step], auto_reset=True,
-                     out=(self._r_env, self.mb_rewards[step], self.mb_dones[step]))
-            env.build_obs(out=self._slot(step + 1) if step + 1 < T else self.next_obs)
+            # step + the next observations in one launch (MAPPO/trainer.py:229-286)
+            env.step_obs(self.mb_actions[step], auto_reset=True,
+                         out=(self._r_env, self.mb_rewards[step], self.mb_dones[step]),
+                         obs_out=self._slot(step + 1) if step + 1 < T else self.next_obs)
         if dev_offset:
             check(lib().mdl_counter_add(ptr(self._off_dev), T, stream_handle(env.device)), "mdl_counter_add")
         next_value = critic(self.next_obs["critic_map"], self.next_obs["critic_vec"]).reshape(E)

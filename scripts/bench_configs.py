@@ -119,8 +119,20 @@ def run(cfg, steps, warmup):
         out["obs_roofline"] = {"achieved_GBs": obs_bytes / (obs_us * 1e-6) / 1e9,
                                "frac": obs_bytes / (obs_us * 1e-6) / 1e9 / HBM}
         both = timed(lambda k: (env.step(acts[k % G]), env.build_obs(out=bufs)), max(20, steps // 5))
-        out["step_plus_obs_us"] = both
-        out["agent_steps_per_s_with_obs"] = E * A / (both * 1e-6)
+        out["step_plus_obs_eager_us"] = both
+        # hipGraph-replayed: step + build_obs as two launches, and mdl_step_obs (one launch)
+        both_g = graph_timed(lambda k: (env.step(acts[k % G], out=(r, sh, dn)), env.build_obs(out=bufs)), 10,
+                             max(1, steps // 50))
+        try:
+            fused_g = graph_timed(lambda k: env.step_obs(acts[k % G], out=(r, sh, dn), obs_out=bufs), 10,
+                                  max(1, steps // 50))
+        except AttributeError:   # an older profiling build without mdl_step_obs (same-box A/B)
+            fused_g = float("nan")
+        out["step_plus_obs_us"] = both_g
+        out["step_obs_fused_us"] = fused_g
+        out["agent_steps_per_s_with_obs"] = E * A / (fused_g * 1e-6)
+        out["step_obs_roofline"] = {"achieved_GBs": (obs_bytes + step_bytes) / (fused_g * 1e-6) / 1e9,
+                                    "frac": (obs_bytes + step_bytes) / (fused_g * 1e-6) / 1e9 / HBM}
     out.update(config=cfg, envs=E, agents=A, packages=P, T=T, groups=groups)
     print(json.dumps(out), flush=True)
     env.close()

@@ -149,12 +149,9 @@ def main():
     def one(k):
         env.step(acts[k % G], auto_reset=True, out=(r, sh, dn))
 
-    # warmup (eager)
-    for k in range(args.warmup):
-        one(k)
-    torch.cuda.synchronize()
-
-    # capture G steps in a hipGraph (torch's stream capture covers the ctypes launches)
+    # capture G steps in a hipGraph (torch's stream capture covers the ctypes launches);
+    # done before the warmup, so that the warmup steps run right before the timed region
+    # (the capture keeps the GPU idle for milliseconds)
     graph = None
     if not args.no_graph:
         s = torch.cuda.Stream(device=dev)
@@ -171,6 +168,11 @@ def main():
         # buffers, packet templates) and must not land inside the timed region
         graph.replay()
         torch.cuda.synchronize()
+
+    # warmup (eager steps, the same kernel)
+    for k in range(args.warmup):
+        one(k)
+    torch.cuda.synchronize()
 
     def barrier():
         if dist is not None:

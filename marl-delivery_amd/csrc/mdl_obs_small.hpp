@@ -104,10 +104,11 @@ __device__ inline void emit_flat4(const uint32_t* FB, int n, float* dst) {
     const uint32_t sh = (uint32_t)(lane & 7) << 2;
     const uint32_t* src = FB + (lane >> 3);
     GLOBAL char* base = (GLOBAL char*)dst;   // wave-uniform base + 32-bit lane offset
-    for (int q = lane; q < nq; q += WAVE, src += 8) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    int q = lane;
+    for (; q < nq; q += WAVE, src += 8) {
         const uint32_t b = __builtin_amdgcn_ubfe(*src, sh, 4u);
         const uint32_t y = (b * 0x204081u) & 0x01010101u;   // bit i -> byte i (no carries: b < 16)
-        typedef float f32x4 __attribute__((ext_vector_type(4)));
         *(GLOBAL f32x4*)(base + ((uint32_t)q << 4)) = f32x4{cvt_ubyte<0>(y), cvt_ubyte<1>(y), cvt_ubyte<2>(y),
                                                             cvt_ubyte<3>(y)};
     }

@@ -25,6 +25,13 @@
 // Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
 // reward, 2 the tracker update, 4 movement, 8 package actions, 16 the move-validity
 // reload, 32 the shaping agent loops, 64 the carried-package gather.  0 in the product.
+// Nearest waiting package of every agent from LDS-packed candidates (1) or one wave
+// reduction per agent (0) -- for the exact-A kernel of many robots (AU = 16, config 5:
+// 24.1 -> 22.1 us per step); with A <= 8 the LDS round trips on the latency-bound
+// path cost more than the reductions they replace (config 2 4.48 -> 4.60 us, measured)
+#ifndef MDL_NEAR_LDS
+#define MDL_NEAR_LDS 1
+#endif
 #ifndef MDL_ABLATE
 #define MDL_ABLATE 0
 #endif
@@ -681,6 +688,55 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                 // order keys < 0x800, slots < 1024): the minimum names the nearest
                 // package with the reference's tie-break and carries its slot
                 uint64_t q = ballot(need_near || need_idle);
+                if constexpr (AU > 8 && MDL_NEAR_LDS) {
+                    // Every agent at once: the waiting candidates of tracker_prev are packed
+                    // into the wave's LDS slice (the reset scratch, unused until a reset below)
+                    // as {start cell, key bits}; lane l scans every (64/AP)-th candidate for
+                    // agent l % AP, and a butterfly over the lane groups leaves agent a's
+                    // minimum on lane a.  A few VALU ops per candidate and group instead of one
+                    // wave reduction per agent and package chunk.
+                    static_assert(AU <= 16, "agents of one lane group");
+                    constexpr int AP = AU <= 8 ? 8 : 16, LG = AU <= 8 ? 3 : 4;
+                    uint64_t* cand = (uint64_t*)(smem + (size_t)wave * lds_stride);
+                    int nw = 0;
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        const int idx = nw + popc64(wvm[c] & lanemask_lt());
+                        if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo[c] << 32);
+                        nw += popc64(wvm[c]);
+                    }
+                    wave_sync();
+                    const int grp = lane >> LG;
+                    const int pa = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, pcell);
+                    uint32_t kmin = 0xffffffffu;
+                    for (int i0 = 0; i0 < nw; i0 += 64 / AP) {   // wave-uniform trip count
+                        const int i = i0 + grp;
+                        const uint64_t ce = cand[i < nw ? i : nw - 1];   // a repeat of the last: harmless for a min
+                        const uint32_t key = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
+                        kmin = key < kmin ? key : kmin;
+                    }
+                    uint32_t o;
+                    if constexpr (AP == 8) {
+                        o = xor_lane<8>(kmin);
+                        kmin = o < kmin ? o : kmin;
+                    }
+                    o = xor_lane<16>(kmin);
+                    kmin = o < kmin ? o : kmin;
+                    o = xor_lane<32>(kmin);
+                    kmin = o < kmin ? o : kmin;
+                    // the nearest candidate's start cell, from its slot's lane
+                    const int js = (int)(kmin & 1023u);
+                    int bc = __builtin_amdgcn_ds_bpermute((js & 63) << 2, stc[0]);
+#pragma unroll
+                    for (int c = 1; c < NCH; c++) {
+                        const int v = __builtin_amdgcn_ds_bpermute((js & 63) << 2, stc[c]);
+                        bc = (js >> 6) == c ? v : bc;
+                    }
+                    const bool found = act && kmin != 0xffffffffu;
+                    Midle = lmask(found && (kmin >> 21) <= 3u);
+                    best_cell = found ? bc : -1;
+                    q = 0;
+                }
                 if constexpr (NCH == 1) {
                     // two agents per pass: their minima interleave
                     for (; q & (q - 1); q &= q - 1, q &= q - 1) {

@@ -9,7 +9,7 @@ import re
 
 def kernel_body(text, sym):
     i = text.index("\n" + sym + ":") + 1
-    j = text.index("s_endpgm", i)
+    j = text.index(".Lfunc_end", i)   # the whole function (a kernel may have several s_endpgm)
     return text[i:j]
 
 

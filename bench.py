@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--fused-k", type=int, default=100, help="bench mode (ii): steps per fused launch (0 = skip)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches only (PMC profiling passes)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend under torchrun (gloo: rehearse N ranks on fewer GPUs)")
     ap.add_argument("--graph-only", action="store_true",
                     help="skip the eager and isolated-launch legs (rocprof kernel-trace pass: the trace then holds "
                          "only the warmup and the timed graph replay, so its average is the timed region's)")
@@ -112,8 +114,12 @@ def main():
     dist = None
     if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:   # under torchrun: always a process group
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":   # RCCL: one rank per GPU
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:   # gloo (rehearsal of the multi-rank path on fewer GPUs than ranks): ranks share GPUs
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -247,7 +253,8 @@ def main():
         kdur_iso_us = float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]) * 1e3)
 
     if dist is not None:
-        t = torch.tensor([wall, wall_eager or 0.0, wall_f or 0.0], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall, wall_eager or 0.0, wall_f or 0.0], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t[0])
         wall_eager = float(t[1]) if wall_eager is not None else None

@@ -309,3 +309,14 @@ def test_readme_random_agent_anchor():
     assert delivered == ref["random"]["delivered"]
     assert round(float(np.mean(rewards)), 2) == -16.50 and round(float(np.std(rewards)), 2) == 6.24
     assert round(float(np.mean(delivered)), 2) == 13.66
+
+
+@pytest.mark.parametrize("mapname,P,tracker", [("map1.txt", 100, "mappo"), ("map1.txt", 40, "fresh"),
+                                               ("map2.txt", 128, "mappo"), ("map3.txt", 64, "fresh"),
+                                               ("synthetic64.txt", 17, "mappo")])
+def test_vs_oracle_sixteen_robots(mapname, P, tracker):
+    """The 16-robot kernel (config 5's robot count: P <= 128, one or two package chunks),
+    whose shaped reward finds every agent's nearest waiting package from LDS-packed
+    candidates: on map1 sixteen robots share 64 free cells, so equal distances -- and the
+    reference's first-in-tracker-order tie-break -- are the common case."""
+    _oracle_compare(mapname, 24, 16, P, 45, 4200 + P, 100, tracker, check_every=25)

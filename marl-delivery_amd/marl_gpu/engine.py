@@ -265,7 +265,8 @@ class BatchedEnv:
         sequence, MAPPO/trainer.py:229-286), as one launch when A <= 8 and P <= 64: the
         kernel builds the observations from the state the step leaves in registers.
         Bit-identical to ``step(...)`` followed by ``build_obs()``.  The envs must share one
-        map shape.  Returns (r_env, r_shaped, done, obs dict)."""
+        map shape.  Returns (r_env, r_shaped, done, obs dict); without ``obs_out`` the obs
+        tensors are the engine's own buffers, overwritten by the next call."""
         n = self.E
         if actions.dtype is not torch.uint8 or not actions.is_cuda or not actions.is_contiguous() \
                 or actions.get_device() != self._dev or actions.numel() != n * self.A:

@@ -28,6 +28,22 @@ MOVE_CODES = {"S": 0, "L": 1, "R": 2, "U": 3, "D": 4}   # anything else -> 5 (no
 OP_CODES = {"0": 0, "1": 1, "2": 2}                     # anything else -> 3 (no env effect)
 
 
+def _codes_to_device(eng, codes):
+    """Action codes -> the engine's device through a reused pinned staging buffer (no
+    synchronous pageable copy; the previous call's snapshot synchronisation has retired
+    the previous copy, so reuse is safe)."""
+    key = codes.shape
+    cache = eng.__dict__.setdefault("_compat_codes", {})
+    bufs = cache.get(key)
+    if bufs is None:
+        bufs = cache[key] = (torch.empty(key, dtype=torch.uint8, pin_memory=True),
+                             torch.empty(key, dtype=torch.uint8, device=eng.device))
+    h, d = bufs
+    h.numpy()[...] = codes
+    d.copy_(h, non_blocking=True)
+    return d
+
+
 def encode_actions(actions, n_robots):
     """list[(move_str, op_str)] -> packed codes (move | op << 3), env.py:193-195 strings."""
     if len(actions) != n_robots:
@@ -60,7 +76,9 @@ class Package:
 
 
 class _Slot:
-    """Host mirror of one env slot of a BatchedEnv, refreshed after each call."""
+    """Host mirror of one env slot of a BatchedEnv, refreshed after each call.  The
+    ``robots`` / ``packages`` object lists are built on first access after a refresh (the
+    state dict is built from the snapshot arrays directly)."""
 
     def __init__(self, owner, idx):
         self._owner = owner
@@ -68,21 +86,43 @@ class _Slot:
 
     def _refresh(self, snap):
         e = self._idx
-        rob = snap["robots"][e]
-        pk = snap["pkgs"][e]
+        self._rob = snap["robots"][e]
+        self._pk = snap["pkgs"][e]
         self.t = int(snap["t"][e])
         self.total_reward = float(snap["total_reward"][e])
-        self.robots = [Robot((int(r[0]), int(r[1])), int(r[2])) for r in rob]
-        self.packages = [Package((int(p[0]), int(p[1])), int(p[4]), (int(p[2]), int(p[3])), int(p[5]), int(p[6]),
-                                 STATUS_NAMES[int(p[7])]) for p in pk]
+        self._robots = None
+        self._packages = None
+
+    @property
+    def robots(self):
+        if self._robots is None:
+            self._robots = [Robot((r[0], r[1]), r[2]) for r in self._rob.tolist()]
+        return self._robots
+
+    @robots.setter
+    def robots(self, v):
+        self._robots = v
+
+    @property
+    def packages(self):
+        if self._packages is None:
+            self._packages = [Package((p[0], p[1]), p[4], (p[2], p[3]), p[5], p[6], STATUS_NAMES[p[7]])
+                              for p in self._pk.tolist()]
+        return self._packages
+
+    @packages.setter
+    def packages(self, v):
+        self._packages = v
 
     def _state_dict(self):
+        t = self.t
+        pk = self._pk
+        new = pk[pk[:, 4] == t].tolist()   # get_state lists the packages spawned at this t (env.py:133-146)
         return {
-            "time_step": self.t,
+            "time_step": t,
             "map": self.grid,
-            "robots": [(r.position[0] + 1, r.position[1] + 1, r.carrying) for r in self.robots],
-            "packages": [(p.package_id, p.start[0] + 1, p.start[1] + 1, p.target[0] + 1, p.target[1] + 1,
-                          p.start_time, p.deadline) for p in self.packages if p.start_time == self.t],
+            "robots": [(r[0] + 1, r[1] + 1, r[2]) for r in self._rob.tolist()],
+            "packages": [(p[6], p[0] + 1, p[1] + 1, p[2] + 1, p[3] + 1, p[4], p[5]) for p in new],
         }
 
 
@@ -118,7 +158,7 @@ class Environment(_Slot):
     def reset(self):
         ids = None if self.engine.E == 1 else [self._idx]
         self.engine.reset(ids)
-        snap = _snapshot(self.engine)
+        snap = self.engine.host_snapshot()
         self.engine._snap = snap
         self._refresh(snap)
         self.done = False
@@ -132,12 +172,12 @@ class Environment(_Slot):
     def step(self, actions):
         codes = encode_actions(actions, self.n_robots)
         eng = self.engine
-        a = torch.from_numpy(codes).to(eng.device).view(1, -1)
+        a = _codes_to_device(eng, codes.reshape(1, -1))
         ids = None if eng.E == 1 else [self._idx]
-        r, _, d = eng.step(a, env_ids=ids, auto_reset=False, action_format="codes")
-        r_h = float(r.cpu()[0])
-        done = bool(d.cpu()[0])
-        snap = _snapshot(eng)
+        eng.step(a, env_ids=ids, auto_reset=False, action_format="codes", out=eng.snapshot_step_out(1))
+        snap = eng.host_snapshot()
+        r_h = float(snap["r_env"][0])
+        done = bool(snap["done"][0])
         eng._snap = snap
         self._refresh(snap)
         infos = {}
@@ -180,8 +220,7 @@ class Environment(_Slot):
 
 
 def _snapshot(engine: BatchedEnv):
-    s = engine.read_state()
-    return {k: v.cpu().numpy() for k, v in s.items() if k in ("robots", "pkgs", "t", "total_reward")}
+    return engine.host_snapshot()
 
 
 class VectorizedEnv:
@@ -209,8 +248,8 @@ class VectorizedEnv:
                                  seeds[i], _engine=self.engine, _idx=i) for i in range(num_envs)]
         self.num_envs = num_envs
 
-    def _refresh_all(self):
-        snap = _snapshot(self.engine)
+    def _refresh_all(self, snap=None):
+        snap = _snapshot(self.engine) if snap is None else snap
         self.engine._snap = snap
         for env in self.envs:
             env._refresh(snap)
@@ -272,11 +311,12 @@ class VectorizedEnv:
         for rnd in rounds:
             ids = [idx[p] for p in rnd]
             codes = np.stack([encode_actions(actions[p], self.envs[e].n_robots) for p, e in zip(rnd, ids)])
-            a = torch.from_numpy(codes).to(eng.device)
-            r, _, d = eng.step(a, env_ids=None if full else ids, auto_reset=False, action_format="codes")
-            r_h = r.cpu().numpy()
-            d_h = d.cpu().numpy().astype(bool)
-            self._refresh_all()
+            a = _codes_to_device(eng, codes)
+            eng.step(a, env_ids=None if full else ids, auto_reset=False, action_format="codes",
+                     out=eng.snapshot_step_out(len(ids)))
+            snap = eng.host_snapshot()
+            r_h, d_h = snap["r_env"], snap["done"].astype(bool)
+            self._refresh_all(snap)
             for k, (p, e) in enumerate(zip(rnd, ids)):
                 env = self.envs[e]
                 info = {}

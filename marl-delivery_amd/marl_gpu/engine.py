@@ -445,6 +445,58 @@ class BatchedEnv:
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         check(lib().mdl_load_state(self._h, buf.ctypes.data, buf.nbytes, self._stream()), "mdl_load_state")
 
+    def _snap_buffers(self):
+        """One device buffer holding the dict-API snapshot (robots, pkgs, t, total_reward) and
+        the step outputs (r_env, r_shaped, done) as typed views, and its pinned host twin:
+        a whole call comes back in ONE copy."""
+        if getattr(self, "_snapbuf", None) is None:
+            E, A, P = self.E, self.A, self.P
+            # int32 words, f64 fields 8-byte aligned
+            sizes = [("robots", E * A * 3, torch.int32), ("pkgs", E * P * 8, torch.int32), ("t", E, torch.int32),
+                     ("total_reward", 2 * E, torch.float64), ("r_env", 2 * E, torch.float64),
+                     ("r_shaped", E, torch.float32), ("done", (E + 3) // 4, torch.uint8)]
+            off, lay = 0, {}
+            for name, words, dt in sizes:
+                if dt == torch.float64 and off % 2:
+                    off += 1
+                lay[name] = (off, words, dt)
+                off += words
+            dev = torch.zeros(off, dtype=torch.int32, device=self.device)
+            host = torch.empty(off, dtype=torch.int32, pin_memory=True)
+
+            def views(buf):
+                v = {}
+                for name, (o, words, dt) in lay.items():
+                    w = buf[o:o + words].view(dt)
+                    v[name] = w[:E] if name == "done" else w
+                v["robots"] = v["robots"].view(E, A, 3)
+                v["pkgs"] = v["pkgs"].view(E, P, 8)
+                return v
+            self._snapbuf = (dev, host, views(dev), views(host))
+        return self._snapbuf
+
+    def snapshot_step_out(self, n=None):
+        """(r_env, r_shaped, done) device views inside the snapshot buffer: pass them as
+        ``step(..., out=...)`` and ``host_snapshot`` returns them with the state."""
+        v = self._snap_buffers()[2]
+        n = self.E if n is None else n
+        cache = self.__dict__.setdefault("_snap_out_views", {})
+        if n not in cache:   # the same view objects per n: the output-buffer check runs once
+            cache[n] = (v["r_env"][:n], v["r_shaped"][:n], v["done"][:n])
+        return cache[n]
+
+    def host_snapshot(self):
+        """The dict-API layer's per-call view: robots [E,A,3] (r, c, carry), pkgs [E,P,8],
+        t [E], total_reward [E], and the last step's outputs written into
+        ``snapshot_step_out`` views (r_env, r_shaped, done) -- exported into one device
+        buffer and copied back in ONE transfer with one stream synchronisation."""
+        dev, host, vd, vh = self._snap_buffers()
+        check(lib().mdl_read_state(self._h, vd["robots"].data_ptr(), vd["pkgs"].data_ptr(), vd["t"].data_ptr(),
+                                   vd["total_reward"].data_ptr(), None, None, self._stream()), "mdl_read_state")
+        host.copy_(dev, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return {k: v.numpy().copy() for k, v in vh.items()}
+
     def read_state(self):
         """int32/f64 device tensors: robots [E,A,3] (r,c,carry), pkgs [E,P,8]
         (sr,sc,tr,tc,start_time,deadline,id,status), t [E], total_reward [E],

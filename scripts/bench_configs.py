@@ -1,5 +1,6 @@
 """Secondary measurements for BASELINE.json configs 3-5 (single GPU slices).
 
+  --config 1   map1, A=5, ONE env driven through the dict API by a random agent (plumbing)
   --config 3   map1, A=5, E=16384: step + full observation build every step
                (actor 6ch map + vector 52 (MO=4, MP=5), critic 4ch map + vector 1301)
   --config 3b  as 3 with the 1007-dim actor vector (MO=MP=100)
@@ -220,6 +221,36 @@ def run_greedy(steps):
     env.close()
 
 
+def run_config1(seconds=5.0):
+    """BASELINE.json configs[0]: map1, 5 agents, ONE env, a random agent driving the dict
+    API (randomagent.py: np.random.choice over moves and ops per robot) -- plumbing, not a
+    throughput path.  Here the env is marl_gpu.compat.Environment (every step a kernel
+    launch plus the dict snapshot back to the host); reference on CPU: 62,184 agent-steps/s
+    with the agent's time, 243,360 env time only (measured in the build
+    container).  Settings of SURVEY.md 8(d) row 1: np.random.seed(2025), env seed 2025,
+    P = 50, T = 500, reset on done."""
+    from marl_gpu.compat import Environment
+    env = Environment("map1.txt", max_time_steps=500, n_robots=5, n_packages=50, seed=2025)
+    env.reset()
+    np.random.seed(2025)
+    moves, ops = ["U", "D", "L", "R", "S"], ["0", "1", "2"]
+    n, t_env, t0 = 0, 0.0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        acts = [(np.random.choice(moves), np.random.choice(ops)) for _ in range(5)]
+        t1 = time.perf_counter()
+        _, _, done, _ = env.step(acts)
+        if done:
+            env.reset()
+        t_env += time.perf_counter() - t1
+        n += 1
+    wall = time.perf_counter() - t0
+    print(json.dumps({"config": "1", "envs": 1, "agents": 5, "steps": n,
+                      "agent_steps_per_s_with_agent": 5 * n / wall, "agent_steps_per_s_env_only": 5 * n / t_env,
+                      "us_per_step_env": t_env / n * 1e6,
+                      "note": "compat.Environment (GPU engine, one env) + the reference random agent's action "
+                              "draws; reference on CPU: 62,184 / 243,360 agent-steps/s (BASELINE.md)"}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="3,3b,4,5")
@@ -228,7 +259,9 @@ def main():
     a = ap.parse_args()
     torch.cuda.set_device(0)
     for c in a.config.split(","):
-        if c in ("rollout", "rollout_graph"):
+        if c == "1":
+            run_config1()
+        elif c in ("rollout", "rollout_graph"):
             run_rollout(a.steps, graph=c == "rollout_graph")
         elif c == "alt":
             run_alt(a.steps)

@@ -21,7 +21,7 @@ import ctypes as C
 import numpy as np
 import torch
 
-from ._lib import check, lib, ptr, stream_handle
+from ._lib import check, lib, stream_handle
 from .engine import MAPPO_SHAPING, QMIX_SHAPING, BatchedEnv
 from .compat import MOVE_CODES, OP_CODES
 
@@ -64,14 +64,57 @@ def pack_view(t, robots1, tracker_rows, H, W, map_index=0) -> np.ndarray:
     return np.concatenate([head, rb.reshape(-1), rows.reshape(-1)]).astype(np.int32)
 
 
-def _upload(blobs):
-    offs = np.zeros(len(blobs), np.int64)
-    pos = 0
-    for i, b in enumerate(blobs):
-        offs[i] = pos
-        pos += b.size
-    flat = np.concatenate(blobs) if blobs else np.zeros(1, np.int32)
-    return torch.from_numpy(flat).cuda(), torch.from_numpy(offs).cuda()
+class _Xfer:
+    """Pinned staging of one helper call: the packed inputs go up in ONE host-to-device copy
+    and every output comes back in ONE device-to-host copy, with one synchronisation (the
+    buffers grow on demand and are reused: each call has retired its transfers on return)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.h_in = self.d_in = self.d_out = self.h_out = None
+
+    @staticmethod
+    def _grow(n):
+        return 1 << max(10, (int(n) - 1).bit_length())
+
+    def up(self, words: np.ndarray) -> torch.Tensor:
+        n = words.size
+        if self.h_in is None or self.h_in.numel() < n:
+            m = self._grow(n)
+            self.h_in = torch.empty(m, dtype=torch.int32, pin_memory=True)
+            self.d_in = torch.empty(m, dtype=torch.int32, device=self.device)
+        self.h_in.numpy()[:n] = words
+        self.d_in[:n].copy_(self.h_in[:n], non_blocking=True)
+        return self.d_in
+
+    def out(self, n: int) -> torch.Tensor:
+        if self.d_out is None or self.d_out.numel() < n:
+            m = self._grow(n)
+            self.d_out = torch.empty(m, dtype=torch.float32, device=self.device)
+            self.h_out = torch.empty(m, dtype=torch.float32, pin_memory=True)
+        return self.d_out
+
+    def down(self, n: int) -> np.ndarray:
+        self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return self.h_out.numpy()[:n].copy()
+
+
+def _xfer(eng) -> _Xfer:
+    x = eng.__dict__.get("_helper_xfer")
+    if x is None:
+        x = eng._helper_xfer = _Xfer(eng.device)
+    return x
+
+
+def _layout(parts):
+    """Word offsets of consecutive parts, each starting at a multiple of its alignment (words)."""
+    offs, pos = [], 0
+    for size, align in parts:
+        pos = (pos + align - 1) // align * align
+        offs.append(pos)
+        pos += size
+    return offs, pos
 
 
 def features(state, tracker_rows, agent_indices, T, MO, MP, MR, MPs, want=("obs", "vec", "gmap", "gvec")):
@@ -81,23 +124,28 @@ def features(state, tracker_rows, agent_indices, T, MO, MP, MR, MPs, want=("obs"
     H, W = len(grid), len(grid[0])
     view = pack_view(state["time_step"], state["robots"], tracker_rows, H, W)
     n = len(agent_indices)
-    views, offs = _upload([view] * n)
-    idx = torch.as_tensor(np.asarray(agent_indices, np.int32)).cuda()
-    dev = views.device
-    out = {}
-    if "obs" in want:
-        out["obs"] = torch.empty((n, 6, H, W), dtype=torch.float32, device=dev)
-    if "vec" in want:
-        out["vec"] = torch.empty((n, 6 + 5 * MO + 5 * MP + 1), dtype=torch.float32, device=dev)
-    if "gmap" in want:
-        out["gmap"] = torch.empty((n, 4, H, W), dtype=torch.float32, device=dev)
-    if "gvec" in want:
-        out["gvec"] = torch.empty((n, 6 * MR + 7 * MPs + 1), dtype=torch.float32, device=dev)
+    x = _xfer(eng)
+    # inputs: n copies of the view, their int64 offsets, the agent indices -- one upload
+    (o_v, o_o, o_i), nin = _layout([(view.size * n, 1), (2 * n, 2), (n, 1)])
+    words = np.zeros(nin, np.int32)
+    words[o_v:o_v + view.size * n] = np.tile(view, n)
+    words[o_o:o_o + 2 * n] = (np.arange(n, dtype=np.int64) * view.size).view(np.int32)
+    words[o_i:o_i + n] = np.asarray(agent_indices, np.int32)
+    din = x.up(words)
+    base_in = din.data_ptr()
+    # outputs: one float buffer, each output 16-B aligned -- one download
+    sizes = {"obs": 6 * H * W, "vec": 6 + 5 * MO + 5 * MP + 1, "gmap": 4 * H * W, "gvec": 6 * MR + 7 * MPs + 1}
+    names = [k for k in ("obs", "vec", "gmap", "gvec") if k in want]
+    offs, nout = _layout([(n * sizes[k], 4) for k in names])
+    dout = x.out(nout)
+    ptrs = {k: dout.data_ptr() + 4 * o for k, o in zip(names, offs)}
     ns = int(np.asarray(tracker_rows).reshape(-1, 8).shape[0])
-    check(lib().mdl_views_features(eng._h, ptr(views), ptr(offs), n, ns, ptr(idx), int(T), MO, MP, MR, MPs,
-                                   ptr(out.get("obs")), ptr(out.get("vec")), ptr(out.get("gmap")),
-                                   ptr(out.get("gvec")), C.c_void_p(stream_handle())), "mdl_views_features")
-    return {k: v.cpu().numpy() for k, v in out.items()}
+    check(lib().mdl_views_features(eng._h, base_in + 4 * o_v, base_in + 4 * o_o, n, ns, base_in + 4 * o_i, int(T),
+                                   MO, MP, MR, MPs, ptrs.get("obs"), ptrs.get("vec"), ptrs.get("gmap"),
+                                   ptrs.get("gvec"), C.c_void_p(stream_handle())), "mdl_views_features")
+    host = x.down(nout)
+    shapes = {"obs": (n, 6, H, W), "vec": (n, sizes["vec"]), "gmap": (n, 4, H, W), "gvec": (n, sizes["gvec"])}
+    return {k: host[o:o + n * sizes[k]].reshape(shapes[k]) for k, o in zip(names, offs)}
 
 
 def convert_observation(env_state_dict, persistent_packages_for_env, current_robot_idx):
@@ -129,18 +177,26 @@ def shaped_rewards_views(g, prev_t, prev_robots1, cur_t, cur_robots1, action_cod
     cr = np.asarray(cur_robots1, np.int64).reshape(-1, 3).copy()
     cr[:, :2] -= 1
     cur = np.concatenate([[cur_t, cr.shape[0]], cr.reshape(-1)]).astype(np.int32)
-    pv, po = _upload([prev])
-    cv, co = _upload([cur])
-    acts = torch.from_numpy(np.asarray(action_codes, np.uint8)).cuda()
-    ao = torch.zeros(1, dtype=torch.int64, device=acts.device)
-    gg = torch.tensor([float(g)], dtype=torch.float64, device=acts.device)
-    out = torch.empty(1, dtype=torch.float32, device=acts.device)
-    cs = (C.c_double * 9)(*[float(x) for x in consts])
+    codes = np.asarray(action_codes, np.uint8).reshape(-1)
+    cw = (codes.size + 3) // 4
+    x = _xfer(eng)
+    # one upload: prev view, cur view, action bytes, three int64 offsets (all 0), g (fp64)
+    (o_p, o_c, o_a, o_off, o_g), nin = _layout([(prev.size, 1), (cur.size, 1), (cw, 1), (6, 2), (2, 2)])
+    words = np.zeros(nin, np.int32)
+    words[o_p:o_p + prev.size] = prev
+    words[o_c:o_c + cur.size] = cur
+    ab = np.zeros(4 * cw, np.uint8)
+    ab[:codes.size] = codes
+    words[o_a:o_a + cw] = ab.view(np.int32)
+    words[o_g:o_g + 2] = np.array([float(g)], np.float64).view(np.int32)
+    b = x.up(words).data_ptr()
+    out = x.out(1)
+    cs = (C.c_double * 9)(*[float(v) for v in consts])
     ns = int(np.asarray(tracker_rows).reshape(-1, 8).shape[0])
-    check(lib().mdl_views_shaped_reward(eng._h, ptr(pv), ptr(po), ns, ptr(cv), ptr(co), ptr(acts), ptr(ao),
-                                        ptr(gg), 1, cs, ptr(out), C.c_void_p(stream_handle())),
-          "mdl_views_shaped_reward")
-    return np.float32(out.cpu().numpy()[0])
+    check(lib().mdl_views_shaped_reward(eng._h, b + 4 * o_p, b + 4 * o_off, ns, b + 4 * o_c, b + 4 * o_off,
+                                        b + 4 * o_a, b + 4 * o_off, b + 4 * o_g, 1, cs, out.data_ptr(),
+                                        C.c_void_p(stream_handle())), "mdl_views_shaped_reward")
+    return np.float32(x.down(1)[0])
 
 
 def compute_shaped_rewards(global_reward, prev_env_state_dict, current_env_state_dict, actions_taken_for_all_agents,

@@ -79,7 +79,13 @@ int mdl_seed(MdlEngine* eng, const uint32_t* seeds, void* stream);
 int mdl_reset(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream);
 int mdl_tracker_clear(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream);
 
-/* One transition for env_ids[0..n) (NULL = all E in order).
+/* env_ids (here and in mdl_reset / mdl_tracker_clear / mdl_step_fused / the greedy entry
+ * points): a DEVICE int32 array of n ids, each processed once and in parallel, so the ids
+ * must be unique and in [0, E); an id outside [0, E) is skipped by the kernels (it cannot
+ * touch another env or allocation), duplicates race.  NULL = all E envs in order.  The
+ * Python layer checks host-side id lists (list semantics, duplicates refused) before upload.
+ *
+ * One transition for env_ids[0..n) (NULL = all E in order).
  * Environment.step (env.py:173-306) + compute_shaped_rewards
  * (MAPPO/helper.py:257-369, evaluated with the pre-step tracker) + the
  * tracker update (MAPPO/trainer.py:95-130) + optional reset-on-done

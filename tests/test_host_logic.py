@@ -1,0 +1,79 @@
+"""Host-side logic that needs no GPU: the dict API's index semantics
+(QMIX/env_vectorized.py:13-37 loops over ``self.envs[i]``), the helper layer's packing
+and transfer layout, and the bench's strong / weak sharding arithmetic."""
+import numpy as np
+import pytest
+
+from marl_gpu import compat
+from marl_gpu import helper as H
+from marl_gpu import dist as D
+
+
+def _venv(n):
+    v = object.__new__(compat.VectorizedEnv)
+    v.num_envs = n
+    return v
+
+
+def test_index_follows_list_indexing():
+    v = _venv(4)
+    assert v._index([0, 3, -1, -4]) == [0, 3, 3, 0]
+    with pytest.raises(IndexError):
+        v._index([4])
+    with pytest.raises(IndexError):
+        v._index([-5])
+    with pytest.raises(TypeError):
+        v._index([1.0])
+    assert v._index(np.array([2, -2])) == [2, 2]
+
+
+def test_rounds_keep_list_order_of_repeated_envs():
+    # the k-th occurrence of an env goes to launch k; launches hold distinct envs
+    idx = [2, 2, 1, 2, 0, 1]
+    rounds = compat.VectorizedEnv._rounds(idx)
+    assert rounds == [[0, 2, 4], [1, 5], [3]]
+    for r in rounds:
+        envs = [idx[p] for p in r]
+        assert len(envs) == len(set(envs))
+    # every position exactly once, and each env's positions in increasing launch order
+    flat = sorted(p for r in rounds for p in r)
+    assert flat == list(range(len(idx)))
+    assert compat.VectorizedEnv._rounds([]) == []
+    assert compat.VectorizedEnv._rounds([0, 1, 2]) == [[0, 1, 2]]
+
+
+def test_encode_actions_codes_and_length_check():
+    codes = compat.encode_actions([("S", "0"), ("L", "1"), ("R", "2"), ("U", "x"), ("D", "0"), ("?", "1")], 6)
+    assert codes.tolist() == [0, 1 | 8, 2 | 16, 3 | 24, 4, 5 | 8]
+    with pytest.raises(ValueError):
+        compat.encode_actions([("S", "0")], 2)
+
+
+def test_layout_aligns_parts():
+    offs, total = H._layout([(3, 1), (4, 2), (5, 4), (1, 1)])
+    assert offs == [0, 4, 8, 13] and total == 14
+    assert H._layout([]) == ([], 0)
+
+
+def test_pack_view_layout_and_checks():
+    v = H.pack_view(7, [(1, 1, 0), (2, 3, 5)], np.array([[5, 1, 0, 0, 1, 1, 0, 9]]), 4, 4)
+    assert v.dtype == np.int32
+    assert v[:4].tolist() == [7, 2, 1, 0]
+    assert v[4:10].tolist() == [0, 0, 0, 1, 2, 5]          # robots 0-indexed
+    assert v[10:].tolist() == [5, 1, 0, 0, 1, 1, 0, 9]
+    with pytest.raises(ValueError):
+        H.pack_view(0, [(5, 1, 0)], np.zeros((0, 8)), 4, 4)  # robot outside the map
+    with pytest.raises(ValueError):
+        H.pack_view(0, [(1, 1, 0)], np.array([[1, 1, 0, 0, 7, 1, 0, 9]]), 4, 4)  # package cell outside
+
+
+def test_shards_cover_every_env_once():
+    for total, world in ((4096, 8), (1000, 3), (7, 8)):
+        seen = []
+        for r in range(world):
+            ids, seeds = D.shard_strong(total, r, world, 42)
+            seen += list(ids)
+            assert list(seeds) == [42 + i for i in ids]
+        assert sorted(seen) == list(range(total))
+    ids, seeds = D.shard(4096, 3, 42)
+    assert ids[0] == 3 * 4096 and len(ids) == 4096 and seeds[0] == 42 + 3 * 4096

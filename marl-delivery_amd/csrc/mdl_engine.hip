@@ -83,6 +83,22 @@ struct DeviceGuard {
     }
 };
 
+// Waves per workgroup of the step kernel for a launch over n envs.  A batch that fills the
+// chip in one round of at least 4 waves per CU runs as ONE workgroup per CU (4..16 waves:
+// fewer workgroups to dispatch; config 2's 4096 envs = 16 waves on each of 256 CUs,
+// 4.47 -> 4.40 us per step); larger batches keep 4-wave workgroups, which finish and free
+// their CU slot independently (16-wave workgroups measured 6-12 % slower at 8192 and 16384
+// envs).  Capped by the LDS budget (the reset scratch per wave).
+int step_wpb(int n, int n_cu, size_t lds_per_wave, int P) {
+    int w = 4;
+    if (P <= 128 && n_cu > 0 && n >= 4 * n_cu && n <= 16 * n_cu) w = (n + n_cu - 1) / n_cu;   // 1024-thread bound: NCH <= 2
+    if (lds_per_wave > 0) {
+        const int cap = (int)(LDS_BUDGET / lds_per_wave);
+        if (w > cap) w = cap;
+    }
+    return w < 1 ? 1 : w;
+}
+
 int waves_per_block(size_t lds_per_wave) {
     if (lds_per_wave == 0) return 4;
     size_t w = LDS_BUDGET / lds_per_wave;
@@ -100,6 +116,7 @@ struct MdlEngine {
     std::vector<void*> allocs;
     size_t lds_step = 0, lds_obs = 0;
     int wpb_step = 1, wpb_obs = 1;
+    int n_cu = 0;   // compute units of the device (step_wpb)
     int maxHW = 0;
     bool seeded = false;
     uint64_t map_fp = 0;  // FNV-1a of every map's (H, W, cells, env_map): checkpoint compatibility
@@ -388,6 +405,10 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
 
     eng->lds_step = mdl::step_lds((int)P);
     eng->wpb_step = waves_per_block(eng->lds_step);
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) eng->n_cu = prop.multiProcessorCount;
+    }
     p.obs_plane_words = mdl::obs_plane_words((int)A, eng->maxHW);
     p.obs_small = mdl::obs_use_small((int)A, (int)P, p.key7_dsh, eng->maxHW) && !getenv("MDL_OBS_GENERIC");
     eng->lds_obs = p.obs_small ? mdl::obs_lds_small((int)A, eng->maxHW)
@@ -462,7 +483,7 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
     if (n == 0) return 0;
     DeviceGuard dg(eng->device);
     HIPCHK(mdl::launch_step(eng->p, actions, action_format, env_ids, n, auto_reset, r_env, r_shaped, done,
-                            eng->wpb_step, eng->lds_step, (hipStream_t)stream));
+                            step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, (hipStream_t)stream));
     return 0;
 }
 
@@ -489,7 +510,7 @@ int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, 
         }
     }
     HIPCHK(mdl::launch_step(eng->p, actions, action_format, nullptr, E, auto_reset, r_env, r_shaped, done,
-                            eng->wpb_step, eng->lds_step, s));
+                            step_wpb(E, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, s));
     HIPCHK(mdl::launch_obs(eng->p, 0, E, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs, eng->lds_obs, s));
     return 0;
 }
@@ -506,7 +527,7 @@ int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format
     if (n == 0) return 0;
     DeviceGuard dg(eng->device);
     HIPCHK(mdl::launch_step_fused(eng->p, actions, action_format, env_ids, n, k_steps, auto_reset, r_env, r_shaped,
-                                  done, eng->wpb_step, eng->lds_step, (hipStream_t)stream));
+                                  done, step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, (hipStream_t)stream));
     return 0;
 }
 

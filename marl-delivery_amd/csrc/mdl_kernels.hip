@@ -287,7 +287,9 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 // one launch with the state held in registers between them; actions [K][n][A],
 // outputs [K][n].  FUSED=false is the API's one step per launch (K = 1).
 #ifndef MDL_STEP_WPB
-#define MDL_STEP_LB 256
+// up to 16 waves per workgroup (the engine's step_wpb) for the one- and two-chunk package
+// tables (<= 61 VGPRs); the larger ones keep 256-thread workgroups and their registers
+#define MDL_STEP_LB (NCH <= 2 ? 1024 : 256)
 #else
 #define MDL_STEP_LB (64 * MDL_STEP_WPB)
 #endif
@@ -1378,10 +1380,8 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
     // checks both at creation)
 #ifdef MDL_STEP_WPB  // profiling builds only: workgroup shape experiments
     wpb = MDL_STEP_WPB;
-    const int threads = 64 * wpb;
-#else
-    const int threads = 256;
 #endif
+    const int threads = 64 * wpb;
 #ifdef MDL_EXP_NOLDS  // profiling builds only: no LDS request (valid only while no env resets)
     lds = 0;
 #endif

@@ -502,7 +502,7 @@ int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, 
     hipStream_t s = (hipStream_t)stream;
     if (eng->p.obs_small && eng->p.A <= 8 && eng->p.P <= 64) {
         const size_t lds = std::max(eng->lds_step, eng->lds_obs);   // one slice: reset scratch, then the planes
-        const int wpb = waves_per_block(lds);
+        const int wpb = step_wpb(E, eng->n_cu, lds, eng->p.P);
         if (wpb >= 1) {
             HIPCHK(mdl::launch_step_obs(eng->p, actions, action_format, E, auto_reset, r_env, r_shaped, done,
                                         actor_map, actor_vec, critic_map, critic_vec, wpb, lds, s));

@@ -933,7 +933,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
 
 // mdl_step_obs: k_step + k_obs_small in one launch (full batch, NCH = 1, A <= 8)
 template <bool STALE, int AU>
-__global__ __launch_bounds__(256) void k_step_obs(const uint32_t* __restrict__ rob_pre,
+__global__ __launch_bounds__(1024) void k_step_obs(const uint32_t* __restrict__ rob_pre,
                                                   const uint64_t* __restrict__ pkg_pre,
                                                   const uint16_t* __restrict__ pst_pre,
                                                   const u32x4* __restrict__ es_pre,
@@ -1452,7 +1452,7 @@ hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, 
     a.lds_stride = (int)lds;
     a.K = 1;
     const ObsArgs o{amap, avec, cmap, cvec};
-    const dim3 grid(blocks_for(n, wpb)), block(256);
+    const dim3 grid(blocks_for(n, wpb)), block(64 * wpb);
     const uint32_t ap = (uint32_t)p.A | ((uint32_t)p.P << 16);
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a, o

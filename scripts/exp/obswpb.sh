@@ -1,5 +1,7 @@
 #!/bin/bash
 # Observation builder workgroup shape (build B with MDL_OBS_LB=1024): 4 / 8 / 16 waves per workgroup vs build A.
+# (The MDL_OBS_LB / MDL_OBS_WPB build knobs were removed after this experiment: no shape was
+# consistently faster, and the run showed the box's bimodal write-bandwidth state)
 set -u
 for rep in 1 2; do
   for V in A B4 B8 B16; do

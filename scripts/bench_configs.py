@@ -168,9 +168,8 @@ def run_rollout(steps, graph=False):
     dt = time.perf_counter() - t0
     out = {"config": "rollout_graph" if graph else "rollout", "envs": E, "agents": A, "rollout_steps": Tr, "rollouts": n,
            "us_per_env_step": dt / (n * Tr) * 1e6, "agent_steps_per_s": E * A * n * Tr / dt,
-           "note": "MappoRollout.collect: linear actor/critic (torch), on-device sampling, mdl_step_obs (step + next "
-                           "observations in one launch) "
-                   "into the rollout buffers, GAE kernel"}
+           "note": "MappoRollout.collect: linear actor/critic (torch), on-device sampling, mdl_step_obs (step + "
+                   "next observations in one launch) into the rollout buffers, GAE kernel"}
     print(json.dumps(out))
 
 

@@ -571,11 +571,27 @@ __device__ inline float np_sum_lanes_dpp(float v) {
     return rdlf(t, AU - 1);
 }
 
+// np_sum_lanes for exactly 16 values on lanes 0..15 as four DPP adds in numpy's pairwise
+// order (n = 16: r_j = x_j + x_{j+8}, then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), no tail;
+// x + y == y + x exactly): row_ror:8, quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_ror:4.
+template <int CTL>
+__device__ __forceinline__ float dppf(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTL, 0xf, 0xf, true));
+}
+__device__ inline float np_sum16_dpp(float v) {
+    const float r = v + dppf<0x128>(v);   // lane j < 8: x_j + x_{j+8}
+    const float s = r + dppf<0xB1>(r);    // even lanes: r_j + r_{j+1}
+    const float c = s + dppf<0x4E>(s);    // lanes 0, 4: (r0+r1)+(r2+r3), (r4+r5)+(r6+r7)
+    const float d = c + dppf<0x124>(c);   // lane 0: the two halves
+    return 0.0f + rdlf(d, 0);
+}
+
 // the step kernel's sum: unrolled form for AU > 0 robots, the general one otherwise
 // (the step kernel's lane values are sums or masked +0.0f: never -0.0f)
 template <int AU>
 __device__ inline float np_sum_step(float v, int n) {
     if constexpr (AU > 0 && AU <= 7) return np_sum_lanes_dpp<AU>(v);
+    else if constexpr (AU == 16) return np_sum16_dpp(v);   // the exact-A kernel: n == 16
     else if constexpr (AU == 8) return np_sum_lanes8<AU>(v, n);
     else return np_sum_lanes(v, n);
 }

@@ -25,6 +25,10 @@
 // Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
 // reward, 2 the tracker update, 4 movement, 8 package actions, 16 the move-validity
 // reload, 32 the shaping agent loops, 64 the carried-package gather.  0 in the product.
+// Movement tests of the 16-robot kernel by lane groups and ds_bpermute (1) or by readlanes (0)
+#ifndef MDL_MOVE_PERM
+#define MDL_MOVE_PERM 1
+#endif
 // Nearest waiting package of every agent from LDS-packed candidates (1) or one wave
 // reduction per agent (0) -- for the exact-A kernel of many robots (AU = 16, config 5:
 // 24.1 -> 22.1 us per step); with A <= 8 the LDS round trips on the latency-bound
@@ -510,7 +514,36 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
             // blocked: a lower-index mover proposes the same cell; occ: the robot
             // now standing on the proposed cell (robots stand on distinct cells)
             int blocked = 0, occ = -1;
-            if constexpr (AU > 0) {
+            if constexpr (AU == 16 && MDL_MOVE_PERM) {
+                // Sixteen robots: lane l tests robot i = l & 15 against robots j = 4g..4g+3
+                // (g = l >> 4, the lane group), fetched by ds_bpermute; two butterfly steps
+                // (lane ^ 16, lane ^ 32) combine the four groups, so lanes 0..15 end with robot
+                // i's answers -- 8 fetches and ~30 VALU instead of 32 readlanes, 32 compares
+                // and 32 selects.  A mover is a robot whose proposal differs from its cell.
+                const int propx = act ? prop : -2, cellx = act ? cell : -3;
+                const int i = lane & 15, g4 = (lane >> 4) << 2;
+                const int pi = __builtin_amdgcn_ds_bpermute(i << 2, propx);
+                int pjv[4], cjv[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    pjv[k] = __builtin_amdgcn_ds_bpermute((g4 + k) << 2, propx);
+                    cjv[k] = __builtin_amdgcn_ds_bpermute((g4 + k) << 2, cellx);
+                }
+                uint32_t hit = 0;
+                int oc = -1;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int j = g4 + k;
+                    hit |= (uint32_t)((pjv[k] == pi) & (j < i) & (pjv[k] != cjv[k]));
+                    oc = cjv[k] == pi ? j : oc;   // robots stand on distinct cells: one match at most
+                }
+                hit |= xor_lane<16>(hit);
+                oc = max(oc, (int)xor_lane<16>((uint32_t)oc));
+                hit |= xor_lane<32>(hit);
+                oc = max(oc, (int)xor_lane<32>((uint32_t)oc));
+                blocked = hit != 0u;
+                occ = oc;
+            } else if constexpr (AU > 0) {
                 // Every test is one compare of this lane's proposal against a readlane'd
                 // scalar, folded into vector registers (hit bits / occupant index): the
                 // chain never hands a vector result to the scalar unit, whose forwarding

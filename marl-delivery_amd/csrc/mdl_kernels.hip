@@ -25,6 +25,10 @@
 // Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
 // reward, 2 the tracker update, 4 movement, 8 package actions, 16 the move-validity
 // reload, 32 the shaping agent loops, 64 the carried-package gather.  0 in the product.
+// Tracker update of the 16-robot kernel with the carried ids as an LDS bitmask (1) or readlanes (0)
+#ifndef MDL_TRK_LDS
+#define MDL_TRK_LDS 1
+#endif
 // Movement tests of the 16-robot kernel by lane groups and ds_bpermute (1) or by readlanes (0)
 #ifndef MDL_MOVE_PERM
 #define MDL_MOVE_PERM 1
@@ -143,6 +147,25 @@ __device__ inline void tracker_update_regs(uint32_t (&ps)[NCH], uint64_t (&td)[N
         } else {
             for (int i = 0; i < A; i++) carried |= rdl(carry, i) == id;
         }
+        const uint32_t upd = carried ? (ps[c] | PS_TRANSIT) : (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
+        ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
+    }
+}
+
+// The same update with the carried test precomputed: bit c of `carried_bits` (this lane)
+// is set when some robot carries id c * 64 + lane + 1.
+template <int NCH>
+__device__ inline void tracker_update_bits(uint32_t (&ps)[NCH], uint64_t (&td)[NCH], bool (&dirty)[NCH],
+                                           const uint64_t (&pk)[NCH], int P, int t, uint32_t carried_bits) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * WAVE + lane;
+        const bool ins = (j < P) & (pk_st(pk[c]) == t) & !(ps[c] & PS_PRESENT);
+        ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
+        td[c] = ins ? pk[c] : td[c];
+        dirty[c] = dirty[c] || ins;
+        const bool carried = (carried_bits >> c) & 1u;
         const uint32_t upd = carried ? (ps[c] | PS_TRANSIT) : (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
         ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
     }
@@ -862,7 +885,21 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
         // After an update, the present entries in transit are exactly the carried ones; with
         // no pick-up, no drop and no spawn at t1 the update is a no-op, so it is skipped.
         if (STALE && !do_rst && !(MDL_ABLATE & 2) && (tookany | dmask | spawned))
-            tracker_update_regs<NCH, AU>(ps, td, dirty, pk, P, A, carry, t1);
+        {
+            if constexpr (AU == 16 && MDL_TRK_LDS) {
+                // sixteen robots: the carried ids as a per-lane bitmask in the wave's LDS slice
+                // (free again: the shaping's candidates are consumed) -- one atomic OR per robot
+                // instead of 16 readlanes and 16 compares per package chunk
+                uint32_t* cm = (uint32_t*)(smem + (size_t)wave * lds_stride);
+                cm[lane] = 0u;
+                wave_sync();
+                if (act && carry != 0) atomicOr(&cm[(carry - 1) & 63], 1u << ((carry - 1) >> 6));
+                wave_sync();
+                tracker_update_bits<NCH>(ps, td, dirty, pk, P, t1, cm[lane]);
+            } else {
+                tracker_update_regs<NCH, AU>(ps, td, dirty, pk, P, A, carry, t1);
+            }
+        }
 
         // ---- reset on done (MAPPO/trainer.py:230-235) ----
         int t_out = t1;

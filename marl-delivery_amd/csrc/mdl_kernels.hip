@@ -766,22 +766,32 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                     wave_sync();
                     const int grp = lane >> LG;
                     const int pa = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, pcell);
-                    uint32_t kmin = 0xffffffffu;
+                    // the same scan answers "a waiting package starts at my (new) cell" for
+                    // the can-pick-up test: one compare per candidate, ORed over the groups
+                    const int ca = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, cell);
+                    uint32_t kmin = 0xffffffffu, hitc = 0;
                     for (int i0 = 0; i0 < nw; i0 += 64 / AP) {   // wave-uniform trip count
                         const int i = i0 + grp;
-                        const uint64_t ce = cand[i < nw ? i : nw - 1];   // a repeat of the last: harmless for a min
+                        const uint64_t ce = cand[i < nw ? i : nw - 1];   // a repeat of the last: harmless for a min / or
                         const uint32_t key = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
                         kmin = key < kmin ? key : kmin;
+                        hitc |= (uint32_t)((int)(uint32_t)ce == ca);
                     }
                     uint32_t o;
                     if constexpr (AP == 8) {
                         o = xor_lane<8>(kmin);
                         kmin = o < kmin ? o : kmin;
+                        hitc |= xor_lane<8>(hitc);
                     }
                     o = xor_lane<16>(kmin);
                     kmin = o < kmin ? o : kmin;
+                    hitc |= xor_lane<16>(hitc);
                     o = xor_lane<32>(kmin);
                     kmin = o < kmin ? o : kmin;
+                    hitc |= xor_lane<32>(hitc);
+                    // Mcan matters only on lanes with op 1 and no package before or after
+                    // (Mwpick below), i.e. exactly where the per-agent loop would set it
+                    Mcan = lmask(hitc != 0u);
                     // the nearest candidate's start cell, from its slot's lane
                     const int js = (int)(kmin & 1023u);
                     int bc = __builtin_amdgcn_ds_bpermute((js & 63) << 2, stc[0]);
@@ -830,7 +840,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                     Midle = (sel && (kmin >> 21) <= 3u) ? ~0u : Midle;
                     best_cell = sel ? bc : best_cell;
                 }
-                for (uint64_t q = ballot(need_can); q; q &= q - 1) {
+                for (uint64_t q = (AU > 8 && MDL_NEAR_LDS) ? 0ull : ballot(need_can); q; q &= q - 1) {
                     const int a = ffs64(q);
                     const int ca = rdl(cell, a);
                     uint64_t h = 0;

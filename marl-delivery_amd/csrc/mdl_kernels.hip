@@ -756,6 +756,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                     static_assert(AU <= 16, "agents of one lane group");
                     constexpr int AP = AU <= 8 ? 8 : 16, LG = AU <= 8 ? 3 : 4;
                     uint64_t* cand = (uint64_t*)(smem + (size_t)wave * lds_stride);
+                    constexpr int GS = 64 / AP;   // lane groups = candidates per scan step
                     int nw = 0;
 #pragma unroll
                     for (int c = 0; c < NCH; c++) {
@@ -763,35 +764,43 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                         if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo[c] << 32);
                         nw += popc64(wvm[c]);
                     }
+                    // sentinels up to a multiple of 2 GS (key bits ~0: never below a real key;
+                    // cell ~0: no map cell), so the scan needs no bound per candidate and
+                    // takes two candidates per lane and step (two LDS reads in flight)
+                    const int nwg = (nw + 2 * GS - 1) & ~(2 * GS - 1);
+                    if (lane < nwg - nw) cand[nw + lane] = ~0ull;
                     wave_sync();
                     const int grp = lane >> LG;
                     const int pa = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, pcell);
                     // the same scan answers "a waiting package starts at my (new) cell" for
-                    // the can-pick-up test: one compare per candidate, ORed over the groups
+                    // the can-pick-up test: one compare per candidate into a lane mask (the
+                    // OR over candidates on the scalar unit)
                     const int ca = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, cell);
-                    uint32_t kmin = 0xffffffffu, hitc = 0;
-                    for (int i0 = 0; i0 < nw; i0 += 64 / AP) {   // wave-uniform trip count
-                        const int i = i0 + grp;
-                        const uint64_t ce = cand[i < nw ? i : nw - 1];   // a repeat of the last: harmless for a min / or
-                        const uint32_t key = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
-                        kmin = key < kmin ? key : kmin;
-                        hitc |= (uint32_t)((int)(uint32_t)ce == ca);
+                    const uint64_t* cp = cand + grp;
+                    uint32_t kmin = 0xffffffffu;
+                    uint64_t hm = 0;
+                    for (int i0 = 0; i0 < nwg; i0 += 2 * GS) {   // wave-uniform trip count
+                        const uint64_t ce = cp[i0], cf = cp[i0 + GS];
+                        const uint32_t ke = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
+                        const uint32_t kf = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
+                        kmin = min(kmin, min(ke, kf));
+                        hm |= ballot((int)(uint32_t)ce == ca) | ballot((int)(uint32_t)cf == ca);
                     }
                     uint32_t o;
                     if constexpr (AP == 8) {
                         o = xor_lane<8>(kmin);
                         kmin = o < kmin ? o : kmin;
-                        hitc |= xor_lane<8>(hitc);
                     }
                     o = xor_lane<16>(kmin);
                     kmin = o < kmin ? o : kmin;
-                    hitc |= xor_lane<16>(hitc);
                     o = xor_lane<32>(kmin);
                     kmin = o < kmin ? o : kmin;
-                    hitc |= xor_lane<32>(hitc);
+                    // agent a's hit: bit a of the lane groups' masks ORed (AP = 16 here)
+                    static_assert(AP == 16, "the hit fold assumes four groups of 16 lanes");
+                    const uint64_t h16 = (hm | (hm >> 16) | (hm >> 32) | (hm >> 48)) & 0xffffull;
                     // Mcan matters only on lanes with op 1 and no package before or after
                     // (Mwpick below), i.e. exactly where the per-agent loop would set it
-                    Mcan = lmask(hitc != 0u);
+                    Mcan = sel64(h16, 0u, ~0u);
                     // the nearest candidate's start cell, from its slot's lane
                     const int js = (int)(kmin & 1023u);
                     int bc = __builtin_amdgcn_ds_bpermute((js & 63) << 2, stc[0]);

@@ -366,6 +366,15 @@ struct ObsArgs {
 // write-back the wave builds the env's observations of the new state from the registers the
 // step leaves (robots on lanes < A, package j on lane j), as MAPPO/trainer.py:229-286 does
 // after every env.step -- one launch and no state reload instead of k_step + k_obs_small.
+// Sixteen-robot movement test: lane L compares robot L & 15 with robot 4 (L >> 4) + k;
+// the lanes where that partner has the lower index.
+__host__ __device__ constexpr uint64_t move_lt_lanes(int k) {
+    uint64_t m = 0;
+    for (int l = 0; l < 64; l++)
+        if (((l >> 4) << 2) + k < (l & 15)) m |= 1ull << l;
+    return m;
+}
+
 template <bool STALE, int NCH, bool FUSED, int AU, bool OBS>
 __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, const uint64_t* __restrict__ pkg_pre,
                                           const uint16_t* __restrict__ pst_pre, const u32x4* __restrict__ es_pre,
@@ -539,32 +548,31 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
             int blocked = 0, occ = -1;
             if constexpr (AU == 16 && MDL_MOVE_PERM) {
                 // Sixteen robots: lane l tests robot i = l & 15 against robots j = 4g..4g+3
-                // (g = l >> 4, the lane group), fetched by ds_bpermute; two butterfly steps
-                // (lane ^ 16, lane ^ 32) combine the four groups, so lanes 0..15 end with robot
-                // i's answers -- 8 fetches and ~30 VALU instead of 32 readlanes, 32 compares
-                // and 32 selects.  A mover is a robot whose proposal differs from its cell.
-                const int propx = act ? prop : -2, cellx = act ? cell : -3;
+                // (g = l >> 4, the lane group), fetched by ds_bpermute; the four groups' answers
+                // are combined so that lanes 0..15 end with robot i's -- 4 fetches instead of
+                // 32 readlanes, 32 compares and 32 selects.  A mover is a robot whose proposal
+                // differs from its cell.  One word per robot: its proposal if it moves (0xffff otherwise: a non-mover
+                // blocks nobody) | its cell << 16 (0xfffe on lanes >= A), so one fetch per
+                // partner; the "lower-index" test is a constant lane mask per k, and the
+                // blocked hits of the four groups are ORed on the scalar unit.
+                const uint32_t wd = ((act && prop != cell) ? (uint32_t)prop : 0xffffu) |
+                                    ((act ? (uint32_t)cell : 0xfffeu) << 16);
                 const int i = lane & 15, g4 = (lane >> 4) << 2;
-                const int pi = __builtin_amdgcn_ds_bpermute(i << 2, propx);
-                int pjv[4], cjv[4];
+                const uint32_t pi = (uint32_t)__builtin_amdgcn_ds_bpermute(i << 2, act ? prop : 0xfffd);
+                uint32_t wj[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    pjv[k] = __builtin_amdgcn_ds_bpermute((g4 + k) << 2, propx);
-                    cjv[k] = __builtin_amdgcn_ds_bpermute((g4 + k) << 2, cellx);
-                }
-                uint32_t hit = 0;
+                for (int k = 0; k < 4; k++) wj[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((g4 + k) << 2, (int)wd);
+                uint64_t H = 0;
                 int oc = -1;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const int j = g4 + k;
-                    hit |= (uint32_t)((pjv[k] == pi) & (j < i) & (pjv[k] != cjv[k]));
-                    oc = cjv[k] == pi ? j : oc;   // robots stand on distinct cells: one match at most
+                    H |= ballot((wj[k] & 0xffffu) == pi) & move_lt_lanes(k);
+                    oc = (wj[k] >> 16) == pi ? g4 + k : oc;   // robots stand on distinct cells: one match at most
                 }
-                hit |= xor_lane<16>(hit);
                 oc = max(oc, (int)xor_lane<16>((uint32_t)oc));
-                hit |= xor_lane<32>(hit);
                 oc = max(oc, (int)xor_lane<32>((uint32_t)oc));
-                blocked = hit != 0u;
+                const uint64_t h16 = (H | (H >> 16) | (H >> 32) | (H >> 48)) & 0xffffull;
+                blocked = sel64(h16, 0u, 1u) != 0u;
                 occ = oc;
             } else if constexpr (AU > 0) {
                 // Every test is one compare of this lane's proposal against a readlane'd

@@ -39,18 +39,33 @@ STEP_BYTES_PER_ENV = lambda A, P: 9 * A + 10 * P + 41  # SURVEY.md §8(d) / A.7 
 HBM_PEAK_GBS = 8000.0                                     # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+# BASELINE.json configs run by --config (configs[1] is the headline; 4 and 5 are the
+# fixed-size multi-GPU batches, split over the ranks: strong scaling of one global batch)
+CONFIGS = {
+    "2": dict(maps=["map1.txt"], agents=5, packages=50, T=500, total=0,
+              metric="agent-steps/sec (whole node), map1 5-agent 4096 envs, 1/2/4/8 MI355X"),
+    "4": dict(maps=[f"map{i}.txt" for i in range(1, 6)], agents=5, packages=50, T=500, total=65536,
+              metric="agent-steps/sec (whole node), map1-map5 mixed 5-agent 65536 envs, 1/2/4/8 MI355X"),
+    "5": dict(maps=["synthetic64.txt"], agents=16, packages=100, T=500, total=131072,
+              metric="agent-steps/sec (whole node), synthetic 64x64 16-agent 131072 envs, 1/2/4/8 MI355X"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks of the job: must equal WORLD_SIZE (1 without torchrun)")
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS),
+                    help="BASELINE.json config: 2 = map1 4096 envs per GPU (the headline), 4 = 65536 mixed-map "
+                         "envs over all ranks, 5 = 131072 synthetic 64x64 16-agent envs over all ranks")
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--total-envs", type=int, default=0,
                     help="strong scaling: this many envs in total, split over the ranks (0 = weak: --envs per GPU)")
-    ap.add_argument("--map", default="map1.txt")
-    ap.add_argument("--agents", type=int, default=5)
-    ap.add_argument("--packages", type=int, default=50)
-    ap.add_argument("--T", type=int, default=500)
+    ap.add_argument("--map", default=None, help="config 2 only (default map1.txt)")
+    ap.add_argument("--agents", type=int, default=None)
+    ap.add_argument("--packages", type=int, default=None)
+    ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--graph-steps", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget per leg (0 = skip)")
@@ -62,17 +77,28 @@ def parse():
     ap.add_argument("--graph-only", action="store_true",
                     help="skip the eager and isolated-launch legs (rocprof kernel-trace pass: the trace then holds "
                          "only the warmup and the timed graph replay, so its average is the timed region's)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c = CONFIGS[a.config]
+    if a.map is not None and a.config != "2":
+        ap.error("--map applies to config 2 only")
+    a.maps = [a.map] if a.map is not None else c["maps"]
+    a.agents = c["agents"] if a.agents is None else a.agents
+    a.packages = c["packages"] if a.packages is None else a.packages
+    a.T = c["T"] if a.T is None else a.T
+    if c["total"] and a.total_envs == 0:
+        a.total_envs = c["total"]
+    a.metric = c["metric"]
+    return a
 
 
-def cpu_baseline(args, grid, seeds0, budget_s, n_threads):
-    """The oracle's C restatement on the same workload: the first rank's envs,
-    same seeds and the same action stream, for as many steps as fit in
-    ~budget_s of wall time, on `n_threads` OpenMP threads (envs split
-    statically across threads, SURVEY.md §8(d) CPU leg (ii))."""
+def cpu_baseline(args, grid, seeds0, budget_s, n_threads, E, map_name):
+    """The oracle's C restatement on the same workload: the first rank's first
+    same-map run of E envs, same seeds, uniform trainer-int actions, for as many
+    steps as fit in ~budget_s of wall time, on `n_threads` OpenMP threads (envs
+    split statically across threads, SURVEY.md §8(d) CPU leg (ii))."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
-    E, A = args.envs, args.agents
+    A = args.agents
     ob = O.OracleBatch(E, grid, A, args.packages, args.T, seed_base=int(seeds0), clear_on_reset=False)
     gen = torch.Generator().manual_seed(0)
     t_all = 0.0
@@ -93,8 +119,8 @@ def cpu_baseline(args, grid, seeds0, budget_s, n_threads):
         pass
     how = "single thread" if n_threads == 1 else f"{n_threads} OpenMP threads"
     return {"value": E * A * steps / t_all, "unit": "agent-steps/s", "cores": n_threads, "kind": "port",
-            "sample": f"{E} envs x {steps} steps ({E * A * steps} agent-steps, {t_all:.1f} s) of the same workload, "
-                      f"oracle/mdl_oracle.c, {how}, host {cpu_model}"}
+            "sample": f"{E} envs ({map_name}) x {steps} steps ({E * A * steps} agent-steps, {t_all:.1f} s) of the "
+                      f"same workload, oracle/mdl_oracle.c, {how}, host {cpu_model}"}
 
 
 def cpu_threads():
@@ -111,6 +137,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:   # one process per GPU: N GPUs need N ranks (torch.distributed.run)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; run N > 1 as "
+                         f"python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}")
     dist = None
     if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:   # under torchrun: always a process group
         import torch.distributed as dist
@@ -126,21 +155,26 @@ def main():
 
     import marl_gpu
     from marl_gpu.maps import grid_array, load_map, map_path
-    grid = grid_array(load_map(map_path(args.map)))
+    grids = [grid_array(load_map(map_path(m))) for m in args.maps]
     A, P = args.agents, args.packages
     from marl_gpu import dist as D
-    if args.total_envs > 0:   # strong scaling: the ranks split one batch (lower ranks take the remainder)
-        ids, _ = D.shard_strong(args.total_envs, rank, world, args.seed)
+    # global env g is seeded args.seed + g (MAPPO/env_vectorized.py:8-9); each rank's ids are contiguous
+    if len(grids) > 1:        # config 4: map groups back to back, dealt to ranks in contiguous blocks
+        ids, seeds, env_map, runs = D.shard_mixed(args.total_envs, len(grids), rank, world, args.seed)
         E_all = args.total_envs
+    elif args.total_envs > 0:   # strong scaling: the ranks split one batch (lower ranks take the remainder)
+        ids, seeds = D.shard_strong(args.total_envs, rank, world, args.seed)
+        env_map, runs, E_all = None, [(0, 0, len(ids))], args.total_envs
     else:
-        ids, _ = D.shard(args.envs, rank, args.seed)
-        E_all = args.envs * world
+        ids, seeds = D.shard(args.envs, rank, args.seed)
+        env_map, runs, E_all = None, [(0, 0, len(ids))], args.envs * world
     E = len(ids)
     if E == 0:
         raise SystemExit(f"bench.py: rank {rank} has no envs (--total-envs {args.total_envs} < {world} ranks)")
-    seed0 = args.seed + ids[0]                                    # global env index -> seed (contiguous ids)
-    env = marl_gpu.BatchedEnv(grid, E, A, P, args.T, seed=seed0, tracker="mappo", shaping="mappo",
-                              max_packages_obs=5, device=dev)
+    obs_dims = dict(max_other_robots=15, max_packages_obs=20, max_robots_state=16, max_packages_state=100) \
+        if args.config == "5" else dict(max_packages_obs=5)
+    env = marl_gpu.BatchedEnv(grids if len(grids) > 1 else grids[0], E, A, P, args.T, seeds=seeds, env_map=env_map,
+                              tracker="mappo", shaping="mappo", device=dev, **obs_dims)
     env.reset()
 
     G = max(1, min(args.graph_steps, args.steps))
@@ -265,21 +299,29 @@ def main():
     if rank == 0:
         per_launch_bytes = STEP_BYTES_PER_ENV(A, P) * E
         achieved = per_launch_bytes / (kdur_us * 1e-6) / 1e9
-        traffic = None
+        traffic, traffic_rec = None, None
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("config") == {"envs": E, "agents": A, "packages": P, "map": args.map}:
-                    traffic = tj.get("hbm_bytes_per_launch")
+                want = {"envs": E, "agents": A, "packages": P, "maps": args.maps}
+                for rec in tj.get("records", []):
+                    if rec.get("config") == want:
+                        traffic, traffic_rec = rec.get("hbm_bytes_per_launch"), rec
             except (OSError, ValueError):
                 traffic = None
         cpu = cpu1 = None
         if world == 1 and args.cpu_seconds > 0:
             nt = cpu_threads()
-            cpu = cpu_baseline(args, grid, seed0, args.cpu_seconds, nt)
-            cpu1 = cpu if nt == 1 else cpu_baseline(args, grid, seed0, args.cpu_seconds, 1)
+            m0, b0, n0 = runs[0]
+            Ec = min(n0, 4096)   # the first same-map run, at most 4096 envs (a bounded sample)
+            cpu = cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, nt, Ec, args.maps[m0])
+            cpu1 = cpu if nt == 1 else cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, 1, Ec, args.maps[m0])
+        kname = {"2": "mdl::k_step<true, 1, false, 5>", "4": "mdl::k_step<true, 1, false, 5> (mixed maps)",
+                 "5": "mdl::k_step<true, 2, false, 16>"}[args.config] if (A, P) == (CONFIGS[args.config]["agents"],
+                                                                              CONFIGS[args.config]["packages"]) \
+            else "mdl::k_step"
         out = {
-            "metric": "agent-steps/sec (whole node), map1 5-agent 4096 envs, 1/2/4/8 MI355X",
+            "metric": args.metric,
             "value": value,
             "unit": "agent-steps/s",
             "n_gpus": world,
@@ -292,17 +334,21 @@ def main():
             "vs_baseline": None,
             "dtype": "int32+fp64",
             "data": "synthetic: uniform random trainer-int actions (Philox, on device), env seeds 42+global index",
-            "config": {"workload": f"{args.map} A={A} P={P} T={args.T} {E} envs/GPU, mdl_step "
+            "config": {"workload": f"BASELINE config {args.config}: {'+'.join(args.maps)} A={A} P={P} T={args.T} "
+                                   f"{E} envs/GPU, mdl_step "
                                    "(move+packages+env reward+MAPPO shaped reward+tracker+auto-reset), "
                                    + ("eager launches" if graph is None else "hipGraph replay"),
                        "envs_per_gpu": E, "total_envs": E_all, "agents": A, "packages": P, "max_time_steps": args.T,
+                       "maps": args.maps, "map_runs_rank0": [[args.maps[m], b, n] for m, b, n in runs],
                        "parallelism": f"env-shard x{world}"},
             "gpu_event_ms_per_step": gpu_ms / K,
             "eager": None if wall_eager is None else {"value": total_agent_steps / wall_eager,
                                                        "ms_per_step": wall_eager / K * 1e3},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mdl::k_step<true, 1, false, 5>", "kernel_us": kdur_us,
+                         "traffic_over_algorithmic": None if traffic is None else traffic / per_launch_bytes,
+                         "traffic_source": None if traffic_rec is None else traffic_rec.get("source"),
+                         "kernel": kname, "kernel_us": kdur_us,
                          "kernel_us_isolated_event_pair": kdur_iso_us,
                          "algorithmic_bytes_per_launch": per_launch_bytes},
             "fused_bench_mode": None if wall_f is None else {

@@ -145,6 +145,40 @@ int mdl_views_idq_reward(MdlEngine* eng, const int32_t* prev_views, const int64_
 int mdl_greedy_init(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream);
 int mdl_greedy_actions(MdlEngine* eng, const int32_t* env_ids, int32_t n, uint8_t* actions, void* stream);
 
+/* ---- dict-API mailbox: the per-call path of Environment.step / reset on single envs ----
+ * Environment.step (env.py:173-306) and VectorizedEnv.step / reset(indices) (QMIX/env_vectorized.py:13-37)
+ * return Python dicts per call, so their cost is the host <-> GPU round trip, not the step.  The mailbox
+ * is ONE engine-owned host allocation, fine-grained and mapped into the device: the caller writes action
+ * codes (and env ids) into it, the step kernel reads them from there, an export kernel writes the touched
+ * envs' rows and a completion word into it, and the call spins on that word (no device staging buffers,
+ * no copy-engine transfers, no stream synchronisation).  Row w of every output = the w-th env of the call
+ * (ids[w] with use_ids, else env w).  The pointers stay valid until mdl_destroy; the outputs of a call
+ * are overwritten by the next one.  Calls are synchronous (they return once the rows are in the mailbox). */
+typedef struct {
+    int32_t* seq;          /* completion word (device-written) */
+    uint8_t* codes;        /* in:  [E][A] MDL_ACTION_CODES bytes */
+    int32_t* ids;          /* in:  [E] env ids of the call (unique, in [0, E)) */
+    double* r_env;         /* out: [E] env.step's reward (fp64) */
+    float* r_shaped;       /* out: [E] compute_shaped_rewards (engine tracker) */
+    uint8_t* done;         /* out: [E] */
+    int32_t* robots;       /* out: [E][A][3] (row, col, carrying), 0-indexed */
+    int32_t* pkgs;         /* out: [E][P][8] as mdl_read_state */
+    int32_t* t;            /* out: [E] */
+    double* total_reward;  /* out: [E] */
+    int32_t* rterms;       /* out: [E] reward terms the step added: MDL_RTERM_* bits (0 after a reset) */
+} MdlMailbox;
+#define MDL_RTERM_MOVE 1    /* a move cost (env.py:256) */
+#define MDL_RTERM_ONTIME 2  /* an on-time delivery reward (env.py:288) */
+#define MDL_RTERM_LATE 4    /* a late delivery reward (env.py:291) */
+/* Allocates the mailbox on first use (E-sized sections) and returns its pointers. */
+int mdl_mailbox(MdlEngine* eng, MdlMailbox* out);
+/* mdl_step(codes, MDL_ACTION_CODES, ids or all E) on the mailbox's inputs, then the rows of those envs. */
+int mdl_mail_step(MdlEngine* eng, int32_t n, int32_t use_ids, int32_t auto_reset, void* stream);
+/* mdl_reset of those envs (Environment.reset, env.py:81-125), then their rows. */
+int mdl_mail_reset(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream);
+/* The rows of those envs only (after other engine calls on `stream`). */
+int mdl_mail_export(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream);
+
 /* ---- checkpoint of the engine state ----
  * A versioned host blob: a 56-byte header (magic "MDLSTATE", version, E, A, P, T, tracker mode,
  * map fingerprint) then every state buffer (robots, packages, state words, env records,

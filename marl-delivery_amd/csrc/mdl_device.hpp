@@ -41,9 +41,12 @@ struct MapDesc {
 // Per-env scalars, one 16-byte record (one load / one store per step).
 struct __align__(16) EnvScalars {
     int32_t t;       // Environment.t
-    uint32_t ctr;    // reserved (0)
+    uint32_t ctr;    // RT_* bits: the reward terms the last step added (0 after a reset)
     double total;    // Environment.total_reward (fp64, as the reference's Python float)
 };
+// env.py's step reward starts as the int 0 (env.py:181) and takes the type of what is added to
+// it: move costs (:256), on-time (:288) / late (:291) delivery rewards
+enum : uint32_t { RT_MOVE = 1u, RT_ONTIME = 2u, RT_LATE = 4u };
 
 // Per-package state word (u16): bits 0-1 env status (ST_*), then the persistent
 // tracker's view of the same id (stale mode): present, in_transit, survivor

@@ -129,6 +129,13 @@ struct MdlEngine {
     unsigned char* gstate = nullptr;
     mdl::GreedyLayout glay{};
     bool greedy_stale = false;  // set by loading a checkpoint that has no greedy section
+    // dict-API mailbox (mdl_mailbox / mdl_mail_*): one host-mapped allocation, made on first use
+    void* mail = nullptr;
+    MdlMailbox mbox{};
+    unsigned* mail_ctr = nullptr;      // device: waves of every export so far (mod 2^32)
+    unsigned mail_waves = 0;           // host mirror of *mail_ctr once the last export ended
+    int32_t mail_seq = 0;              // last completion value published
+    std::vector<uint8_t> mail_seen;    // duplicate-id check of a call
 
     // (device pointer, bytes) of every state buffer, in checkpoint order
     // (the greedy agents' records follow when with_greedy: they exist once mdl_greedy_init ran)
@@ -162,6 +169,7 @@ struct MdlEngine {
     }
     ~MdlEngine() {
         for (void* v : allocs) (void)hipFree(v);
+        if (mail) (void)hipHostFree(mail);
     }
 };
 
@@ -502,8 +510,8 @@ int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, 
     hipStream_t s = (hipStream_t)stream;
     if (eng->p.obs_small && eng->p.A <= 8 && eng->p.P <= 64) {
         const size_t lds = std::max(eng->lds_step, eng->lds_obs);   // one slice: reset scratch, then the planes
-        const int wpb = step_wpb(E, eng->n_cu, lds, eng->p.P);
-        if (wpb >= 1) {
+        if (lds <= LDS_BUDGET) {   // else: the two-launch path below
+            const int wpb = step_wpb(E, eng->n_cu, lds, eng->p.P);
             HIPCHK(mdl::launch_step_obs(eng->p, actions, action_format, E, auto_reset, r_env, r_shaped, done,
                                         actor_map, actor_vec, critic_map, critic_vec, wpb, lds, s));
             return 0;
@@ -529,6 +537,119 @@ int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format
     HIPCHK(mdl::launch_step_fused(eng->p, actions, action_format, env_ids, n, k_steps, auto_reset, r_env, r_shaped,
                                   done, step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, (hipStream_t)stream));
     return 0;
+}
+
+// ---- dict-API mailbox: Environment.step / reset with one launch pair and no copies ----
+static_assert(mdl::RT_MOVE == MDL_RTERM_MOVE && mdl::RT_ONTIME == MDL_RTERM_ONTIME && mdl::RT_LATE == MDL_RTERM_LATE,
+              "reward-term bits of the header and the kernels");
+int mdl_mailbox(MdlEngine* eng, MdlMailbox* out) {
+    if (!eng || !out) return fail("mdl_mailbox: null argument");
+    if (!eng->mail) {
+        DeviceGuard dg(eng->device);
+        const size_t E = eng->p.E, A = eng->p.A, P = eng->p.P;
+        // 16-byte aligned sections: seq | codes | ids | r_env | r_shaped | done | robots | pkgs | t | total | rterms
+        const size_t sz[11] = {16, E * A, E * 4, E * 8, E * 4, E, E * A * 12, E * P * 32, E * 4, E * 8, E * 4};
+        size_t off[11], tot = 0;
+        for (int i = 0; i < 11; i++) {
+            off[i] = tot;
+            tot += (sz[i] + 15) & ~(size_t)15;
+        }
+        // fine-grained (coherent) and mapped: the kernels read the inputs and write the rows in place,
+        // the host reads them as soon as the completion word changes
+        HIPCHK(hipHostMalloc(&eng->mail, tot, hipHostMallocCoherent | hipHostMallocMapped));
+        memset(eng->mail, 0, tot);
+        char* b = (char*)eng->mail;
+        MdlMailbox& m = eng->mbox;
+        m.seq = (int32_t*)(b + off[0]);
+        m.codes = (uint8_t*)(b + off[1]);
+        m.ids = (int32_t*)(b + off[2]);
+        m.r_env = (double*)(b + off[3]);
+        m.r_shaped = (float*)(b + off[4]);
+        m.done = (uint8_t*)(b + off[5]);
+        m.robots = (int32_t*)(b + off[6]);
+        m.pkgs = (int32_t*)(b + off[7]);
+        m.t = (int32_t*)(b + off[8]);
+        m.total_reward = (double*)(b + off[9]);
+        m.rterms = (int32_t*)(b + off[10]);
+        if (eng->alloc(&eng->mail_ctr, 1)) return -1;
+        eng->mail_seen.assign(E, 0);
+    }
+    *out = eng->mbox;
+    return 0;
+}
+
+namespace {
+// The ids of a mailbox call (host memory, so checked here): in [0, E), no repeats.
+int mail_check_ids(MdlEngine* eng, int32_t n, int32_t use_ids, const char* who) {
+    if (!eng->mail) return fail("%s: call mdl_mailbox first", who);
+    if (n < 0 || n > eng->p.E || (!use_ids && n != eng->p.E))
+        return fail("%s: n=%d (use_ids=%d) out of range for %d envs", who, n, use_ids, eng->p.E);
+    if (!use_ids) return 0;
+    const int32_t* ids = eng->mbox.ids;
+    int rc = 0;
+    for (int i = 0; i < n && !rc; i++) {
+        const int32_t e = ids[i];
+        if (e < 0 || e >= eng->p.E) rc = fail("%s: env id %d out of range [0, %d)", who, e, eng->p.E);
+        else if (eng->mail_seen[e]) rc = fail("%s: env id %d listed twice", who, e);
+        else eng->mail_seen[e] = 1;
+    }
+    for (int i = 0; i < n; i++)
+        if (ids[i] >= 0 && ids[i] < eng->p.E) eng->mail_seen[ids[i]] = 0;
+    return rc;
+}
+
+// export the call's rows into the mailbox, then wait (spinning) for the completion word
+int mail_finish(MdlEngine* eng, int32_t n, int32_t use_ids, hipStream_t s, const char* who) {
+    const MdlMailbox& m = eng->mbox;
+    const int32_t want = eng->mail_seq = (eng->mail_seq % 0x7ffffff0) + 1;
+    mdl::MailRows rows{m.seq, m.robots, m.pkgs, m.t, m.total_reward, m.rterms};
+    const unsigned base = eng->mail_waves;
+    eng->mail_waves += mdl::mail_export_waves(n);   // the device counter's value after this launch
+    HIPCHK(mdl::launch_mail_export(eng->p, use_ids ? m.ids : nullptr, n, rows, eng->mail_ctr, base, want, s));
+    volatile const int32_t* seq = m.seq;
+    for (unsigned long spins = 1;; spins++) {
+        if (*seq == want) break;
+        __builtin_ia32_pause();
+        if ((spins & 0xffff) == 0) {   // a failed launch never publishes: ask the stream now and then
+            const hipError_t q = hipStreamQuery(s);
+            if (q != hipSuccess && q != hipErrorNotReady) return fail("%s: %s", who, hipGetErrorString(q));
+            if (q == hipSuccess && *seq != want) return fail("%s: the export finished without publishing", who);
+        }
+    }
+    return 0;
+}
+}  // namespace
+
+int mdl_mail_step(MdlEngine* eng, int32_t n, int32_t use_ids, int32_t auto_reset, void* stream) {
+    if (!eng) return fail("mdl_mail_step: null engine");
+    if (!eng->seeded) return fail("mdl_mail_step: engine not seeded (call mdl_seed first)");
+    if (mail_check_ids(eng, n, use_ids, "mdl_mail_step")) return -1;
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    hipStream_t s = (hipStream_t)stream;
+    const MdlMailbox& m = eng->mbox;
+    HIPCHK(mdl::launch_step(eng->p, m.codes, MDL_ACTION_CODES, use_ids ? m.ids : nullptr, n, auto_reset, m.r_env,
+                            m.r_shaped, m.done, step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, s));
+    return mail_finish(eng, n, use_ids, s, "mdl_mail_step");
+}
+
+int mdl_mail_reset(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream) {
+    if (!eng) return fail("mdl_mail_reset: null engine");
+    if (!eng->seeded) return fail("mdl_mail_reset: engine not seeded (call mdl_seed first)");
+    if (mail_check_ids(eng, n, use_ids, "mdl_mail_reset")) return -1;
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(mdl::launch_reset(eng->p, use_ids ? eng->mbox.ids : nullptr, n, eng->wpb_step, eng->lds_step, s));
+    return mail_finish(eng, n, use_ids, s, "mdl_mail_reset");
+}
+
+int mdl_mail_export(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream) {
+    if (!eng) return fail("mdl_mail_export: null engine");
+    if (mail_check_ids(eng, n, use_ids, "mdl_mail_export")) return -1;
+    if (n == 0) return 0;
+    DeviceGuard dg(eng->device);
+    return mail_finish(eng, n, use_ids, (hipStream_t)stream, "mdl_mail_export");
 }
 
 // ---- greedy baseline ----
@@ -570,7 +691,8 @@ int mdl_greedy_init(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* str
     if (greedy_alloc(eng, s)) return -1;
     if (n == 0) return 0;
     HIPCHK(mdl::launch_greedy_init(eng->p, eng->glay, eng->gstate, env_ids, n, s));
-    if (!env_ids) eng->greedy_stale = false;
+    // every env re-initialised: no id list, or a list of E ids (ids are unique by contract)
+    if (!env_ids || n == eng->p.E) eng->greedy_stale = false;
     return 0;
 }
 
@@ -579,7 +701,7 @@ int mdl_greedy_actions(MdlEngine* eng, const int32_t* env_ids, int32_t n, uint8_
     if (!eng->gstate) return fail("mdl_greedy_actions: call mdl_greedy_init first");
     if (eng->greedy_stale)
         return fail("mdl_greedy_actions: the greedy agents' state predates mdl_load_state of a checkpoint without "
-                    "it; call mdl_greedy_init");
+                    "it; call mdl_greedy_init for every env (no id list, or all E ids)");
     if (!env_ids) n = eng->p.E;
     if (n < 0 || n > eng->p.E) return fail("mdl_greedy_actions: n=%d out of range", n);
     if (n == 0) return 0;

@@ -475,6 +475,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
     GLOBAL uint64_t* trkw;
     GLOBAL u32x4* esw;
     const int KK = FUSED ? K : 1;
+    uint32_t rfl = 0;   // the last step's reward terms (EnvScalars::rterms)
     for (int k = 0; k < KK; k++) {
         int mv, op;
         decode_action(araw, fmt_, mv, op);   // every lane (no exec-masked block), then masked
@@ -690,6 +691,9 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
             const int i = ffs64(m);
             rr += ((omask >> i) & 1ull) ? p.delivery_reward : p.delay_reward;
         }
+        // which of env.py's reward terms fired (the reference's r stays the int 0 until one
+        // does, env.py:181,256,288,291): move cost, on-time delivery, late delivery
+        rfl = (n_cost ? RT_MOVE : 0u) | (omask ? RT_ONTIME : 0u) | ((dmask & ~omask) ? RT_LATE : 0u);
         const int t1 = t0 + 1;
         const double total = tot_cur + rr;
 
@@ -1005,7 +1009,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
         }
     }
     if (lane == 0)
-        esw[e] = u32x4{(uint32_t)t_cur, 0u, (uint32_t)__double2loint(tot_cur), (uint32_t)__double2hiint(tot_cur)};
+        esw[e] = u32x4{(uint32_t)t_cur, rfl, (uint32_t)__double2loint(tot_cur), (uint32_t)__double2hiint(tot_cur)};
     STAMP(11);
 #ifdef MDL_STAMPS
     if (lane == 0)
@@ -1436,8 +1440,64 @@ __global__ __launch_bounds__(256) void k_export(DevParams p, int32_t* __restrict
     }
 }
 
+// ------------------------------------------------------- dict-API mailbox export
+// The rows of the envs a dict-API call touched (row w = env ids[w], or env w without ids),
+// written straight into the engine's host-mapped mailbox (no device staging buffer, no copy
+// engine), then one completion word: every wave of the grid counts itself in the running
+// counter `ctr` (never reset: `base` is its value before this launch) after a system-scope
+// release of its stores; the last one publishes `seq`, which the host spins on (mdl_mail_*).
+// Robot / package rows are the k_export layout.
+__global__ __launch_bounds__(256) void k_mail_export(DevParams p, const int32_t* __restrict__ ids, int n,
+                                                     MailRows m, unsigned* __restrict__ ctr, unsigned base,
+                                                     int32_t seq) {
+    const int lane = lane_id();
+    const int w = blockIdx.x * 4 + wave_id();
+    const int A = p.A, P = p.P;
+    int e = -1;
+    if (w < n) e = ids ? uni(ids[w]) : w;
+    if ((unsigned)e < (unsigned)p.E) {
+        if (lane < A) {
+            const uint32_t rv = p.rob[(size_t)e * A + lane];
+            int32_t* o = m.robots + ((size_t)w * A + lane) * 3;
+            o[0] = cell_r(rob_cell(rv));
+            o[1] = cell_c(rob_cell(rv));
+            o[2] = rob_carry(rv);
+        }
+        for (int j = lane; j < P; j += WAVE) {
+            const size_t g = (size_t)e * P + j;
+            const uint64_t d = p.pkg[g];
+            int4* o = (int4*)(m.pkgs + ((size_t)w * P + j) * 8);
+            o[0] = int4{cell_r(pk_start(d)), cell_c(pk_start(d)), cell_r(pk_target(d)), cell_c(pk_target(d))};
+            o[1] = int4{pk_st(d), pk_dl(d), j + 1, (int)(p.pstate[g] & PS_STATUS)};
+        }
+        if (lane == 0) {
+            const EnvScalars s = p.es[e];
+            m.t[w] = s.t;
+            m.total[w] = s.total;
+            m.rterms[w] = (int32_t)s.ctr;
+        }
+    }
+    __atomic_thread_fence(__ATOMIC_RELEASE);   // this wave's mailbox stores, before it is counted
+    if (lane == 0) {
+        const unsigned waves = gridDim.x * 4u;
+        if (atomicAdd(ctr, 1u) - base == waves - 1u) {   // the last wave of the grid: every row is out
+            __atomic_thread_fence(__ATOMIC_ACQ_REL);
+            __hip_atomic_store(m.seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 static int blocks_for(int n, int wpb) { return (n + wpb - 1) / wpb; }
+
+unsigned mail_export_waves(int n) { return 4u * (unsigned)blocks_for(n > 0 ? n : 1, 4); }
+
+hipError_t launch_mail_export(const DevParams& p, const int32_t* ids, int n, const MailRows& m, unsigned* ctr,
+                              unsigned base, int32_t seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_mail_export, dim3(blocks_for(n > 0 ? n : 1, 4)), dim3(256), 0, s, p, ids, n, m, ctr, base,
+                       seq);
+    return hipGetLastError();
+}
 
 static int nch_for(int P) {
     const int c = (P + WAVE - 1) / WAVE;

@@ -32,6 +32,18 @@ hipError_t launch_views_shaped(const DevParams& p, const int32_t* prev, const in
                                const int64_t* cur_offs, const uint8_t* acts, const int64_t* act_offs, const double* g,
                                int n, const ShapingConsts& C, float* out, int wpb, size_t lds, int NSmax,
                                hipStream_t s);
+// the dict-API mailbox's output rows (host-mapped memory; row w = the w-th env of a call)
+struct MailRows {
+    int32_t* seq;      // completion word, written last
+    int32_t* robots;   // [E][A][3]
+    int32_t* pkgs;     // [E][P][8]
+    int32_t* t;        // [E]
+    double* total;     // [E]
+    int32_t* rterms;   // [E] RT_* bits
+};
+unsigned mail_export_waves(int n);   // waves of one k_mail_export launch over n envs
+hipError_t launch_mail_export(const DevParams& p, const int32_t* ids, int n, const MailRows& m, unsigned* ctr,
+                              unsigned base, int32_t seq, hipStream_t s);
 hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int32_t* t, double* total,
                          int32_t* tracker, int32_t* tracker_data, hipStream_t s);
 

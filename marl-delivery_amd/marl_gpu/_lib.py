@@ -45,6 +45,15 @@ class MdlConfig(C.Structure):
     ]
 
 
+MDL_RTERM_MOVE, MDL_RTERM_ONTIME, MDL_RTERM_LATE = 1, 2, 4
+
+
+class MdlMailbox(C.Structure):
+    """include/mdl_engine.h MdlMailbox: host-mapped sections of the dict-API mailbox."""
+    _fields_ = [(n, C.c_void_p) for n in ("seq", "codes", "ids", "r_env", "r_shaped", "done", "robots", "pkgs", "t",
+                                          "total_reward", "rterms")]
+
+
 # name -> (restype, argtypes); every symbol include/mdl_engine.h declares
 _vp, _i32, _i64p = C.c_void_p, C.c_int32, C.c_void_p
 SIGNATURES = {
@@ -62,6 +71,10 @@ SIGNATURES = {
     "mdl_views_idq_reward": (C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp]),
     "mdl_greedy_init": (C.c_int, [_vp, _vp, _i32, _vp]),
     "mdl_greedy_actions": (C.c_int, [_vp, _vp, _i32, _vp, _vp]),
+    "mdl_mailbox": (C.c_int, [_vp, C.POINTER(MdlMailbox)]),
+    "mdl_mail_step": (C.c_int, [_vp, _i32, _i32, _i32, _vp]),
+    "mdl_mail_reset": (C.c_int, [_vp, _i32, _i32, _vp]),
+    "mdl_mail_export": (C.c_int, [_vp, _i32, _i32, _vp]),
     "mdl_state_bytes": (C.c_int, [_vp, C.POINTER(C.c_int64)]),
     "mdl_save_state": (C.c_int, [_vp, _vp, C.c_int64, _vp]),
     "mdl_load_state": (C.c_int, [_vp, _vp, C.c_int64, _vp]),

@@ -4,55 +4,63 @@
 ``reset()`` / ``step()`` / ``get_state()`` dicts, ``render()``) and
 ``VectorizedEnv`` mirrors MAPPO/env_vectorized.py:1-24 plus the ``indices=``
 variant of QMIX/env_vectorized.py:1-49, so agents and trainer loops written
-against the reference run unchanged.  Every transition executes on the GPU;
-the dicts are materialised from a device snapshot after each call.
+against the reference run unchanged.  Every transition executes on the GPU.
+A call goes through the engine's host-mapped mailbox (``BatchedEnv.mailbox``):
+the action codes are written into it, the step kernel reads them there, an
+export kernel writes the touched envs' rows back into it and the call returns
+when they have arrived -- no device staging buffers, copies or stream syncs.
 
-Differences (documented, not silent):
-  * ``step`` returns the int ``0`` whenever the step reward is 0.0 (the
-    reference returns the int 0 when no reward term fired, and a float that
-    happens to equal 0.0 in the rare case the terms cancel);
-  * ``render_pygame`` is a no-op (headless), ``render`` prints text as the
-    reference's ``render``.
+``step`` returns the reward with the reference's type: env.py:181 starts from
+the int ``0`` and adds the move costs / delivery rewards (env.py:256,288,291),
+so the result is the int 0 when no term fired, a float once a float constant
+was added (also when the terms cancel to 0.0), and an int when only int
+constants were added.  ``render_pygame`` is a no-op (headless); ``render``
+prints text as the reference's ``render`` does.
 """
 from __future__ import annotations
 
 import operator
 
 import numpy as np
-import torch
 
+from ._lib import MDL_RTERM_LATE, MDL_RTERM_MOVE, MDL_RTERM_ONTIME
 from .engine import STATUS_NAMES, BatchedEnv
 from .maps import grid_array, load_map, map_path
 
 MOVE_CODES = {"S": 0, "L": 1, "R": 2, "U": 3, "D": 4}   # anything else -> 5 (no move, != 'S')
 OP_CODES = {"0": 0, "1": 1, "2": 2}                     # anything else -> 3 (no env effect)
+# the code byte of every (move, op) string pair: move | op << 3
+_PAIR_CODES = {(m, o): mc | (oc << 3) for m, mc in list(MOVE_CODES.items()) for o, oc in list(OP_CODES.items())}
 
 
-def _codes_to_device(eng, codes):
-    """Action codes -> the engine's device through a reused pinned staging buffer (no
-    synchronous pageable copy; the previous call's snapshot synchronisation has retired
-    the previous copy, so reuse is safe)."""
-    key = codes.shape
-    cache = eng.__dict__.setdefault("_compat_codes", {})
-    bufs = cache.get(key)
-    if bufs is None:
-        bufs = cache[key] = (torch.empty(key, dtype=torch.uint8, pin_memory=True),
-                             torch.empty(key, dtype=torch.uint8, device=eng.device))
-    h, d = bufs
-    h.numpy()[...] = codes
-    d.copy_(h, non_blocking=True)
-    return d
+def _code(mv, op):
+    c = _PAIR_CODES.get((mv, op)) if isinstance(mv, str) and isinstance(op, str) else None
+    if c is None:
+        c = (MOVE_CODES.get(mv, 5) if isinstance(mv, str) else 5) | \
+            ((OP_CODES.get(op, 3) if isinstance(op, str) else 3) << 3)
+    return c
+
+
+def _encode(actions, n_robots):
+    if len(actions) != n_robots:   # env.py:182-183
+        raise ValueError("The number of actions must match the number of robots.")
+    return [_code(mv, op) for mv, op in actions]
 
 
 def encode_actions(actions, n_robots):
     """list[(move_str, op_str)] -> packed codes (move | op << 3), env.py:193-195 strings."""
-    if len(actions) != n_robots:
-        raise ValueError("The number of actions must match the number of robots.")
-    out = np.empty(n_robots, np.uint8)
-    for i, (mv, op) in enumerate(actions):
-        m = MOVE_CODES.get(mv, 5)
-        out[i] = m | (OP_CODES.get(op, 3) << 3)
-    return out
+    return np.array(_encode(actions, n_robots), np.uint8)
+
+
+def typed_reward(r, rterms, move_cost, delivery_reward, delay_reward):
+    """The value env.step returns, with the reference's type (env.py:181,256,288,291)."""
+    if not rterms:
+        return 0
+    if (rterms & MDL_RTERM_MOVE and isinstance(move_cost, float)) or \
+            (rterms & MDL_RTERM_ONTIME and isinstance(delivery_reward, float)) or \
+            (rterms & MDL_RTERM_LATE and isinstance(delay_reward, float)):
+        return float(r)
+    return int(r)
 
 
 class Robot:
@@ -76,20 +84,19 @@ class Package:
 
 
 class _Slot:
-    """Host mirror of one env slot of a BatchedEnv, refreshed after each call.  The
-    ``robots`` / ``packages`` object lists are built on first access after a refresh (the
-    state dict is built from the snapshot arrays directly)."""
+    """Host mirror of one env slot of a BatchedEnv, refreshed from the mailbox rows after each
+    call that touched it.  The ``robots`` / ``packages`` object lists are built on first access
+    after a refresh (the state dict is built from the row arrays directly)."""
 
     def __init__(self, owner, idx):
         self._owner = owner
         self._idx = idx
 
-    def _refresh(self, snap):
-        e = self._idx
-        self._rob = snap["robots"][e]
-        self._pk = snap["pkgs"][e]
-        self.t = int(snap["t"][e])
-        self.total_reward = float(snap["total_reward"][e])
+    def _set_rows(self, rob, pk, t, total):
+        self._rob = rob
+        self._pk = pk
+        self.t = int(t)
+        self.total_reward = float(total)
         self._robots = None
         self._packages = None
 
@@ -126,6 +133,11 @@ class _Slot:
         }
 
 
+def _rows(mb, n):
+    """Copies of the first n rows of the mailbox's state outputs (the next call overwrites them)."""
+    return mb["robots"][:n].copy(), mb["pkgs"][:n].copy(), mb["t"][:n].tolist(), mb["total_reward"][:n].tolist()
+
+
 class Environment(_Slot):
     """env.py:18-455 on the GPU engine (one env)."""
 
@@ -145,22 +157,28 @@ class Environment(_Slot):
             _engine = BatchedEnv(grid_array(self.grid), 1, n_robots, n_packages, max_time_steps, move_cost,
                                  delivery_reward, delay_reward, seeds=[seed], tracker="fresh")
             _engine._grid_list = self.grid
-            self._vec = None
+            mb = _engine.mailbox()
+            _engine.mail_export(1, False)       # the constructor's layout (env.py:41)
+            rob, pk, t, tot = _rows(mb, 1)
+            self._set_rows(rob[0], pk[0], t[0], tot[0])
         super().__init__(_engine, _idx)
         self.engine = _engine
+        self._mb = _engine.mailbox()
+        self._single = _engine.E == 1
         self.done = False
         self.state = None
-        if getattr(_engine, "_snap", None) is None:
-            _engine._snap = _snapshot(_engine)
-        self._refresh(_engine._snap)
+
+    def _call_one(self, fn):
+        """One mailbox call on this env alone; refreshes this env's rows."""
+        mb = self._mb
+        if not self._single:
+            mb["ids"][0] = self._idx
+        fn(1, not self._single)
+        self._set_rows(mb["robots"][0].copy(), mb["pkgs"][0].copy(), mb["t"][0], mb["total_reward"][0])
 
     # env.py:81-125
     def reset(self):
-        ids = None if self.engine.E == 1 else [self._idx]
-        self.engine.reset(ids)
-        snap = self.engine.host_snapshot()
-        self.engine._snap = snap
-        self._refresh(snap)
+        self._call_one(self.engine.mail_reset)
         self.done = False
         self.state = None
         return self._state_dict()
@@ -170,21 +188,17 @@ class Environment(_Slot):
 
     # env.py:173-306
     def step(self, actions):
-        codes = encode_actions(actions, self.n_robots)
-        eng = self.engine
-        a = _codes_to_device(eng, codes.reshape(1, -1))
-        ids = None if eng.E == 1 else [self._idx]
-        eng.step(a, env_ids=ids, auto_reset=False, action_format="codes", out=eng.snapshot_step_out(1))
-        snap = eng.host_snapshot()
-        r_h = float(snap["r_env"][0])
-        done = bool(snap["done"][0])
-        eng._snap = snap
-        self._refresh(snap)
+        mb = self._mb
+        mb["codes"][0] = _encode(actions, self.n_robots)
+        self._call_one(self.engine.mail_step)
+        done = bool(mb["done"][0])
+        r = typed_reward(mb["r_env"][0], int(mb["rterms"][0]), self.move_cost, self.delivery_reward,
+                         self.delay_reward)
         infos = {}
         if done:
             infos["total_reward"] = self.total_reward
             infos["total_time_steps"] = self.t
-        return self._state_dict(), (0 if r_h == 0.0 else r_h), done, infos
+        return self._state_dict(), r, done, infos
 
     def check_terminate(self):
         if self.t == self.max_time_steps:
@@ -219,10 +233,6 @@ class Environment(_Slot):
         return None
 
 
-def _snapshot(engine: BatchedEnv):
-    return engine.host_snapshot()
-
-
 class VectorizedEnv:
     """MAPPO/env_vectorized.py:1-24 + QMIX ``indices=`` (QMIX/env_vectorized.py:13-37).
 
@@ -238,21 +248,23 @@ class VectorizedEnv:
         n_robots = env_kwargs.get("n_robots", 5)
         n_packages = env_kwargs.get("n_packages", 20)
         T = env_kwargs.get("max_time_steps", 100)
-        self.engine = BatchedEnv(grid_array(grid), num_envs, n_robots, n_packages, T,
-                                 env_kwargs.get("move_cost", -0.01), env_kwargs.get("delivery_reward", 10.),
-                                 env_kwargs.get("delay_reward", 1.), seeds=seeds, tracker="fresh")
+        consts = (env_kwargs.get("move_cost", -0.01), env_kwargs.get("delivery_reward", 10.),
+                  env_kwargs.get("delay_reward", 1.))
+        self.engine = BatchedEnv(grid_array(grid), num_envs, n_robots, n_packages, T, *consts, seeds=seeds,
+                                 tracker="fresh")
         self.engine._grid_list = grid
-        self.engine._snap = None
-        self.envs = [Environment(map_file, T, n_robots, n_packages, env_kwargs.get("move_cost", -0.01),
-                                 env_kwargs.get("delivery_reward", 10.), env_kwargs.get("delay_reward", 1.),
-                                 seeds[i], _engine=self.engine, _idx=i) for i in range(num_envs)]
+        self.envs = [Environment(map_file, T, n_robots, n_packages, *consts, seeds[i], _engine=self.engine, _idx=i)
+                     for i in range(num_envs)]
         self.num_envs = num_envs
+        self._mb = self.engine.mailbox()
+        self.engine.mail_export(num_envs, False)   # every env's constructor layout (env.py:41)
+        self._take_rows(list(range(num_envs)))
 
-    def _refresh_all(self, snap=None):
-        snap = _snapshot(self.engine) if snap is None else snap
-        self.engine._snap = snap
-        for env in self.envs:
-            env._refresh(snap)
+    def _take_rows(self, ids):
+        """Refresh the envs of the last mailbox call (row k = env ids[k])."""
+        rob, pk, t, tot = _rows(self._mb, len(ids))
+        for k, e in enumerate(ids):
+            self.envs[e]._set_rows(rob[k], pk[k], t[k], tot[k])
 
     def _index(self, indices):
         """``self.envs[i]`` semantics of the reference's loops: negatives count from the
@@ -281,15 +293,18 @@ class VectorizedEnv:
         return rounds
 
     def reset(self, indices=None):
+        eng = self.engine
         if indices is None:
-            self.engine.reset(None)
-            self._refresh_all()
+            eng.mail_reset(self.num_envs, False)
+            self._take_rows(list(range(self.num_envs)))
             return [env._state_dict() for env in self.envs]
         idx = self._index(indices)
         out = [None] * len(idx)
         for rnd in self._rounds(idx):
-            self.engine.reset([idx[p] for p in rnd])
-            self._refresh_all()
+            ids = [idx[p] for p in rnd]
+            self._mb["ids"][:len(ids)] = ids
+            eng.mail_reset(len(ids), True)
+            self._take_rows(ids)
             for p in rnd:
                 out[p] = self.envs[idx[p]]._state_dict()
         return out
@@ -303,26 +318,30 @@ class VectorizedEnv:
             rounds = [list(range(len(idx)))]
             full = len(idx) == self.num_envs
         else:
-            idx = self._index(indices)[:len(actions)]
+            # zip(indices, actions): ids past the end of the action list are never looked up
+            idx = self._index(list(indices)[:len(actions)])
             rounds = self._rounds(idx)
             full = False
-        eng = self.engine
+        eng, mb = self.engine, self._mb
         res = [None] * len(idx)
         for rnd in rounds:
             ids = [idx[p] for p in rnd]
-            codes = np.stack([encode_actions(actions[p], self.envs[e].n_robots) for p, e in zip(rnd, ids)])
-            a = _codes_to_device(eng, codes)
-            eng.step(a, env_ids=None if full else ids, auto_reset=False, action_format="codes",
-                     out=eng.snapshot_step_out(len(ids)))
-            snap = eng.host_snapshot()
-            r_h, d_h = snap["r_env"], snap["done"].astype(bool)
-            self._refresh_all(snap)
+            n = len(ids)
+            codes = mb["codes"]
+            for k, (p, e) in enumerate(zip(rnd, ids)):
+                codes[k] = _encode(actions[p], self.envs[e].n_robots)
+            if not full:
+                mb["ids"][:n] = ids
+            eng.mail_step(n, not full)
+            r_h, d_h, rt_h = mb["r_env"][:n].tolist(), mb["done"][:n].tolist(), mb["rterms"][:n].tolist()
+            self._take_rows(ids)
             for k, (p, e) in enumerate(zip(rnd, ids)):
                 env = self.envs[e]
                 info = {}
                 if d_h[k]:
                     info = {"total_reward": env.total_reward, "total_time_steps": env.t}
-                res[p] = (env._state_dict(), 0 if r_h[k] == 0.0 else float(r_h[k]), bool(d_h[k]), info)
+                res[p] = (env._state_dict(), typed_reward(r_h[k], rt_h[k], env.move_cost, env.delivery_reward,
+                                                          env.delay_reward), bool(d_h[k]), info)
         if not res:
             raise ValueError("not enough values to unpack (expected 4, got 0)")   # zip(*[]) in the reference
         states, rewards, dones, infos = (list(x) for x in zip(*res))

@@ -11,6 +11,7 @@ rollout tensors for a single learner.
 """
 from __future__ import annotations
 
+import bisect
 import os
 
 import torch
@@ -37,6 +38,39 @@ def shard_strong(total_envs: int, rank: int, world_size: int, base_seed: int):
     n = per + (1 if rank < rem else 0)
     ids = list(range(first, first + n))
     return ids, [base_seed + i for i in ids]
+
+
+def map_group_sizes(total_envs: int, n_maps: int):
+    """Envs per map of a mixed-map batch laid out as contiguous map groups, the first groups
+    taking the remainder: 65536 envs over map1..map5 -> 13108, 13107, 13107, 13107, 13107
+    (SURVEY.md §8(d) config 4)."""
+    per, rem = divmod(int(total_envs), int(n_maps))
+    return [per + (1 if m < rem else 0) for m in range(n_maps)]
+
+
+def shard_mixed(total_envs: int, n_maps: int, rank: int, world_size: int, base_seed: int):
+    """This rank's part of a mixed-map batch (config 4).
+
+    The global batch is the map groups back to back (``map_group_sizes``); global env g
+    runs map ``env_map[g]`` with seed ``base_seed + g`` -- what one VectorizedEnv-style process
+    would give it (MAPPO/env_vectorized.py:8-9) -- and rank r owns the contiguous global ids
+    ``shard_strong`` deals it, so the map groups are dealt to ranks in contiguous blocks and a
+    rank holds at most a few same-map runs.  Returns (global ids, seeds, local env -> map index,
+    [(map index, first local env, n envs)] of the rank's runs)."""
+    sizes = map_group_sizes(total_envs, n_maps)
+    ids, seeds = shard_strong(total_envs, rank, world_size, base_seed)
+    bounds = [0]
+    for s in sizes:
+        bounds.append(bounds[-1] + s)
+    env_map, runs = [], []
+    for local, g in enumerate(ids):
+        m = bisect.bisect_right(bounds, g) - 1
+        env_map.append(m)
+        if runs and runs[-1][0] == m:
+            runs[-1][2] += 1
+        else:
+            runs.append([m, local, 1])
+    return ids, seeds, env_map, [tuple(r) for r in runs]
 
 
 def max_over_ranks(values, device=None):

@@ -294,7 +294,8 @@ class BatchedEnv:
                                  ptrs[0], ptrs[1], ptrs[2], op["actor_map"], op["actor_vec"], op["critic_map"],
                                  op["critic_vec"], _raw_stream(self._dev)), "mdl_step_obs")
         self._keep = (None, actions)
-        return out[0], out[1], out[2], obs_out
+        # only the outputs written by this call (a cached dict's other entries would be stale)
+        return out[0], out[1], out[2], {k: (v if k in which else None) for k, v in obs_out.items()}
 
     def step_fused(self, actions: torch.Tensor, env_ids=None, auto_reset: bool = True, action_format: str = "int",
                    out=None):
@@ -345,13 +346,14 @@ class BatchedEnv:
                              f"same-shape group (this one ends at env {int(self._shape_run_end[env_begin])})")
         return n, self.grids[int(self.env_map[env_begin])]
 
-    @staticmethod
-    def _check_obs_out(t, name, shape):
+    def _check_obs_out(self, t, name, shape):
         want = 1
         for s in shape:
             want *= s
         if not isinstance(t, torch.Tensor) or t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
             raise TypeError(f"{name} must be a contiguous float32 device tensor")
+        if t.get_device() != self.device.index:
+            raise ValueError(f"{name} must be on {self.device}, not cuda:{t.get_device()}")
         if t.numel() < want:
             raise ValueError(f"{name} holds {t.numel()} floats, needs {want} {tuple(shape)}")
 
@@ -417,8 +419,9 @@ class BatchedEnv:
         ids, n = self._ids(env_ids)
         if out is None:
             out = torch.empty((n, self.A), dtype=torch.uint8, device=self.device)
-        elif out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or out.numel() < n * self.A:
-            raise ValueError(f"out must be a contiguous uint8 device tensor of >= {n}x{self.A} entries")
+        elif out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or out.numel() < n * self.A \
+                or out.get_device() != self.device.index:
+            raise ValueError(f"out must be a contiguous uint8 tensor on {self.device} of >= {n}x{self.A} entries")
         if n == 0:
             return out
         check(lib().mdl_greedy_actions(self._h, ptr(ids), n, ptr(out), self._stream()), "mdl_greedy_actions")
@@ -445,57 +448,51 @@ class BatchedEnv:
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         check(lib().mdl_load_state(self._h, buf.ctypes.data, buf.nbytes, self._stream()), "mdl_load_state")
 
-    def _snap_buffers(self):
-        """One device buffer holding the dict-API snapshot (robots, pkgs, t, total_reward) and
-        the step outputs (r_env, r_shaped, done) as typed views, and its pinned host twin:
-        a whole call comes back in ONE copy."""
-        if getattr(self, "_snapbuf", None) is None:
+    # ---- dict-API mailbox (include/mdl_engine.h: mdl_mailbox / mdl_mail_*) ----
+    def mailbox(self) -> dict:
+        """numpy views of the engine's host-mapped mailbox (allocated on first use): inputs
+        ``codes`` [E, A] (MDL_ACTION_CODES bytes) and ``ids`` [E]; outputs, row w = the w-th env
+        of the last call: ``r_env``, ``r_shaped``, ``done``, ``robots`` [E, A, 3], ``pkgs``
+        [E, P, 8], ``t``, ``total_reward``, ``rterms`` (the MDL_RTERM_* bits of the reward
+        terms the step added).  The device reads the inputs and writes the outputs in place;
+        every ``mail_*`` call returns once its rows are there (it spins on a completion word)."""
+        mb = self.__dict__.get("_mb")
+        if mb is None:
+            m = _lib.MdlMailbox()
+            check(lib().mdl_mailbox(self._h, C.byref(m)), "mdl_mailbox")
             E, A, P = self.E, self.A, self.P
-            # int32 words, f64 fields 8-byte aligned
-            sizes = [("robots", E * A * 3, torch.int32), ("pkgs", E * P * 8, torch.int32), ("t", E, torch.int32),
-                     ("total_reward", 2 * E, torch.float64), ("r_env", 2 * E, torch.float64),
-                     ("r_shaped", E, torch.float32), ("done", (E + 3) // 4, torch.uint8)]
-            off, lay = 0, {}
-            for name, words, dt in sizes:
-                if dt == torch.float64 and off % 2:
-                    off += 1
-                lay[name] = (off, words, dt)
-                off += words
-            dev = torch.zeros(off, dtype=torch.int32, device=self.device)
-            host = torch.empty(off, dtype=torch.int32, pin_memory=True)
 
-            def views(buf):
-                v = {}
-                for name, (o, words, dt) in lay.items():
-                    w = buf[o:o + words].view(dt)
-                    v[name] = w[:E] if name == "done" else w
-                v["robots"] = v["robots"].view(E, A, 3)
-                v["pkgs"] = v["pkgs"].view(E, P, 8)
-                return v
-            self._snapbuf = (dev, host, views(dev), views(host))
-        return self._snapbuf
+            def arr(addr, ctype, shape):
+                n = 1
+                for d in shape:
+                    n *= d
+                return np.ctypeslib.as_array((ctype * n).from_address(addr)).reshape(shape)
+            mb = dict(codes=arr(m.codes, C.c_uint8, (E, A)), ids=arr(m.ids, C.c_int32, (E,)),
+                      r_env=arr(m.r_env, C.c_double, (E,)), r_shaped=arr(m.r_shaped, C.c_float, (E,)),
+                      done=arr(m.done, C.c_uint8, (E,)), robots=arr(m.robots, C.c_int32, (E, A, 3)),
+                      pkgs=arr(m.pkgs, C.c_int32, (E, P, 8)), t=arr(m.t, C.c_int32, (E,)),
+                      total_reward=arr(m.total_reward, C.c_double, (E,)), rterms=arr(m.rterms, C.c_int32, (E,)))
+            self._mb = mb
+            L = lib()
+            self._mail_fns = (L.mdl_mail_step, L.mdl_mail_reset, L.mdl_mail_export)
+        return mb
 
-    def snapshot_step_out(self, n=None):
-        """(r_env, r_shaped, done) device views inside the snapshot buffer: pass them as
-        ``step(..., out=...)`` and ``host_snapshot`` returns them with the state."""
-        v = self._snap_buffers()[2]
-        n = self.E if n is None else n
-        cache = self.__dict__.setdefault("_snap_out_views", {})
-        if n not in cache:   # the same view objects per n: the output-buffer check runs once
-            cache[n] = (v["r_env"][:n], v["r_shaped"][:n], v["done"][:n])
-        return cache[n]
+    def mail_step(self, n: int, use_ids: bool, auto_reset: bool = False) -> None:
+        """Step the mailbox's envs (``ids[:n]`` when use_ids, else all E, with ``codes[:n]``) and
+        bring their rows into the mailbox: one step launch + one export launch, then a spin."""
+        rc = self._mail_fns[0](self._h, n, 1 if use_ids else 0, 1 if auto_reset else 0, _raw_stream(self._dev))
+        if rc:
+            check(rc, "mdl_mail_step")
 
-    def host_snapshot(self):
-        """The dict-API layer's per-call view: robots [E,A,3] (r, c, carry), pkgs [E,P,8],
-        t [E], total_reward [E], and the last step's outputs written into
-        ``snapshot_step_out`` views (r_env, r_shaped, done) -- exported into one device
-        buffer and copied back in ONE transfer with one stream synchronisation."""
-        dev, host, vd, vh = self._snap_buffers()
-        check(lib().mdl_read_state(self._h, vd["robots"].data_ptr(), vd["pkgs"].data_ptr(), vd["t"].data_ptr(),
-                                   vd["total_reward"].data_ptr(), None, None, self._stream()), "mdl_read_state")
-        host.copy_(dev, non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
-        return {k: v.numpy().copy() for k, v in vh.items()}
+    def mail_reset(self, n: int, use_ids: bool) -> None:
+        rc = self._mail_fns[1](self._h, n, 1 if use_ids else 0, _raw_stream(self._dev))
+        if rc:
+            check(rc, "mdl_mail_reset")
+
+    def mail_export(self, n: int, use_ids: bool) -> None:
+        rc = self._mail_fns[2](self._h, n, 1 if use_ids else 0, _raw_stream(self._dev))
+        if rc:
+            check(rc, "mdl_mail_export")
 
     def read_state(self):
         """int32/f64 device tensors: robots [E,A,3] (r,c,carry), pkgs [E,P,8]

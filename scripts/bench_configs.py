@@ -5,7 +5,8 @@
                (actor 6ch map + vector 52 (MO=4, MP=5), critic 4ch map + vector 1301)
   --config 3b  as 3 with the 1007-dim actor vector (MO=MP=100)
   --config 4   map1..map5 mixed, A=5, E=65536/8 per GPU (one GPU's shard), step only
-  --config 5   synthetic 64x64, A=16, P=100, E=131072/8 per GPU, step only
+  --config 5   synthetic 64x64, A=16, P=100, E=131072/8 per GPU, step; full observations per
+               chunk of 1024 envs
   --config rollout / rollout_graph   MAPPO rollout on the device
   --config alt      IDQ/qmix featurizers (§8(f)2)
   --config greedy   batched greedy baseline (§8(f)3)
@@ -134,6 +135,27 @@ def run(cfg, steps, warmup):
         out["agent_steps_per_s_with_obs"] = E * A / (fused_g * 1e-6)
         out["step_obs_roofline"] = {"achieved_GBs": (obs_bytes + step_bytes) / (fused_g * 1e-6) / 1e9,
                                     "frac": (obs_bytes + step_bytes) / (fused_g * 1e-6) / 1e9 / HBM}
+    if cfg == "5":
+        # the full observations (actor 6 x 64 x 64 maps for 16 agents, vectors
+        # MO = 15 / MP = 20, critic map + MR = 16 / MPs = 100 vector) are 1.65 MB per env-step, so they
+        # are built and reported per chunk of envs (general k_obs builder: A > 8, P > 64)
+        H = W = 64
+        chunk = 1024
+        cb = env.obs_buffers(chunk, H, W)
+        per_env = 4 * (A * 6 * H * W + A * env.actor_vec_dim + 4 * H * W + env.critic_vec_dim)
+        for k in range(2):
+            env.build_obs(0, chunk, out=cb)
+        nchunks = E // chunk
+        reps = 2
+        chunk_us = timed(lambda k: env.build_obs((k % nchunks) * chunk, chunk, out=cb), nchunks * reps)
+        out["obs_chunk_envs"] = chunk
+        out["obs_chunk_us"] = chunk_us
+        out["obs_bytes_per_env_step"] = per_env
+        out["obs_chunk_roofline"] = {"achieved_GBs": per_env * chunk / (chunk_us * 1e-6) / 1e9,
+                                     "frac": per_env * chunk / (chunk_us * 1e-6) / 1e9 / HBM}
+        out["obs_all_envs_us"] = chunk_us * nchunks
+        out["agent_steps_per_s_step_plus_obs"] = E * A / ((step_us + chunk_us * nchunks) * 1e-6)
+        del cb
     out.update(config=cfg, envs=E, agents=A, packages=P, T=T, groups=groups)
     print(json.dumps(out), flush=True)
     env.close()

@@ -23,6 +23,7 @@ Fixtures written (all small, compressed):
   kat.json          notebook known-answer test (MAPPO/marl-delivery-mappo.ipynb cell 11)
   eval_anchor.json  evaluation.run_eval('random'/'greedy') per-episode results
                     for the README results table (README.md:117-121)
+  reward_types.npz  env.step's int-vs-float reward (cancelling / int constants)  env.py:181,252-292
   alt_features.npz  IDQ/qmix convert_state, qmix convert_global_state_to_tensor
                     (incl. cropped/padded shapes), IDQ reward_shaping with int
                     and string ops   IDQ/networks.py:112-349, qmix/networks.py:243-468
@@ -583,13 +584,61 @@ def gen_alt_features(ref, quick):
     print("alt feature cases", len(cases))
 
 
+def gen_reward_types(ref, quick):
+    """env.step's reward TYPE (env.py:181 starts ``r = 0``, an int; ``:256,288,291`` add the
+    constants): the int 0 when no term fired, a float once a float constant was added -- also
+    when the terms cancel to 0.0 -- and an int when only int constants fired.  Constants chosen
+    so that cancellations happen (move_cost -0.5: two moves + one late drop = 0.0), plus int
+    delivery / delay rewards.  Ops are biased towards pick-ups and drops."""
+    cases = [
+        # map, A, P, T, seed, act_seed, n, (move_cost, delivery_reward, delay_reward)
+        ("map.txt", 3, 10, 100, 3, 21, 1500, (-0.5, 10.0, 1.0)),
+        ("map.txt", 3, 8, 80, 4, 22, 400, (-0.5, 10, 1)),
+        ("map1.txt", 5, 20, 100, 5, 23, 400, (0, 2.0, 1)),
+        ("map.txt", 2, 6, 70, 6, 24, 400, (-0.25, 0.5, 0.5)),
+    ]
+    if quick:
+        cases = cases[:2]
+    arrays, meta = {}, []
+    for ci, (m, A, P, T, seed, aseed, n, consts) in enumerate(cases):
+        mc, dr, lr = consts
+        env = ref.env.Environment(map_file(m), T, A, P, move_cost=mc, delivery_reward=dr, delay_reward=lr, seed=seed)
+        env.reset()
+        rs = np.random.RandomState(aseed)
+        acts = np.zeros((n, A, 2), np.uint8)   # (move code, op code) per robot
+        r_l, rint_l, done_l = [], [], []
+        for k in range(n):
+            moves = rs.randint(0, 5, size=A)
+            ops = rs.choice(3, size=A, p=[0.2, 0.4, 0.4])
+            actions = [("SLRUD"[mv], str(op)) for mv, op in zip(moves, ops)]
+            acts[k] = [enc_action(*a) for a in actions]
+            _, r, done, _ = env.step(actions)
+            r_l.append(float(r))
+            rint_l.append(isinstance(r, int))
+            done_l.append(bool(done))
+            if done:
+                env.reset()
+        arrays[f"acts_{ci}"] = acts
+        arrays[f"r_{ci}"] = np.array(r_l, np.float64)
+        arrays[f"rint_{ci}"] = np.array(rint_l, np.bool_)
+        arrays[f"done_{ci}"] = np.array(done_l, np.bool_)
+        zf = int(np.sum((~arrays[f"rint_{ci}"]) & (arrays[f"r_{ci}"] == 0.0)))
+        ni = int(np.sum(arrays[f"rint_{ci}"] & (arrays[f"r_{ci}"] != 0.0)))
+        meta.append(dict(map=m, A=A, P=P, T=T, seed=seed, n=n, consts=[mc, dr, lr],
+                         const_types=[type(x).__name__ for x in consts], float_zero_steps=zf, int_nonzero_steps=ni))
+        print("reward types case", ci, "float 0.0 steps", zf, "int non-zero steps", ni)
+    arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "reward_types.npz"), **arrays)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     ref = load_reference()
-    todo = args.only.split(",") if args.only else ["reset", "steps", "mappo", "qmix", "helpers", "kat", "eval", "alt"]
+    todo = args.only.split(",") if args.only else ["reset", "steps", "mappo", "qmix", "helpers", "kat", "eval", "alt",
+                                                   "rtypes"]
     if "reset" in todo:
         gen_reset(ref, args.quick)
     if "steps" in todo:
@@ -611,6 +660,8 @@ def main():
         gen_eval_anchor(ref, args.quick)
     if "alt" in todo:
         gen_alt_features(ref, args.quick)
+    if "rtypes" in todo:
+        gen_reward_types(ref, args.quick)
 
 
 if __name__ == "__main__":

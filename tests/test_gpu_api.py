@@ -150,5 +150,8 @@ def test_vectorized_env_repeated_and_negative_indices():
     # zip semantics: more indices than actions steps only as many envs as there are actions
     s, r, d, i = v1.step([[("S", "0")] * 3], indices=[0, 1])
     assert len(s) == 1
+    # ... and an index past the end of the action list is never looked up (zip), even out of range
+    s, r, d, i = v1.step([[("S", "0")] * 3], indices=[0, 99])
+    assert len(s) == 1
     st = v1.reset(indices=[1, 1])
     assert len(st) == 2

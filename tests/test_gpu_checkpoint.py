@@ -59,6 +59,53 @@ def test_checkpoint_resume_is_exact(tracker, tmp_path):
     assert np.array_equal(blob, np.load(path, allow_pickle=False))
 
 
+@pytest.mark.parametrize("tracker", ["mappo", "fresh"])
+def test_checkpoint_restore_matches_oracle(tracker):
+    """The restored stream against the CPU oracle (the reference cannot checkpoint, so the
+    oracle run from the same seeds through the same actions is the external anchor): an
+    engine restored from a blob taken after 50 steps is stepped through 100 more, across
+    several auto-resets (T = 37: each reset draws from the restored MT19937 states), and its
+    env / shaped rewards, done flags, robot and package state and tracker rows equal the
+    oracle's (MAPPO/trainer.py:194-286 semantics, both tracker modes)."""
+    import oracle as O
+    O.build()
+    mg = _mg()
+    g = grid("map2.txt")
+    E, A, P, T, seed = 48, 5, 50, 37, 123
+    kw = dict(seed=seed, tracker=tracker, shaping="mappo", max_packages_obs=5)
+    a = mg.BatchedEnv(g, E, A, P, T, **kw)
+    a.reset()
+    ob = O.OracleBatch(E, g, A, P, T, seed_base=seed, clear_on_reset=(tracker == "fresh"))
+    rs = np.random.RandomState(11)
+    acts = rs.randint(0, 15, size=(150, E, A)).astype(np.uint8)
+    for k in range(50):
+        a.step(torch.from_numpy(acts[k]).cuda(), auto_reset=True)
+        ob.step(acts[k], auto_reset=True, consts=O.MAPPO_CONSTS)
+    blob = a.save_state()
+    a.close()
+    b = mg.BatchedEnv(g, E, A, P, T, **kw)        # never reset: everything comes from the blob
+    b.load_state(blob)
+    n_done = 0
+    for k in range(50, 150):
+        r, sh, d = b.step(torch.from_numpy(acts[k]).cuda(), auto_reset=True)
+        r0, sh0, d0 = ob.step(acts[k], auto_reset=True, consts=O.MAPPO_CONSTS)
+        np.testing.assert_array_equal(r.cpu().numpy(), r0, err_msg=f"r step {k}")
+        np.testing.assert_array_equal(sh.cpu().numpy(), sh0, err_msg=f"shaped step {k}")
+        np.testing.assert_array_equal(d.cpu().numpy().astype(bool), d0, err_msg=f"done step {k}")
+        n_done += int(d0.sum())
+        if k % 10 == 0 or k == 149:
+            s = snap(b)
+            for e in range(E):
+                os_ = ob.env(e).state()
+                np.testing.assert_array_equal(s["robots"][e], os_["robots"], err_msg=f"robots env {e} step {k}")
+                np.testing.assert_array_equal(s["pkgs"][e], os_["pkgs"], err_msg=f"pkgs env {e} step {k}")
+                assert s["t"][e] == os_["t"] and s["total_reward"][e] == os_["total_reward"], (e, k)
+                np.testing.assert_array_equal(b.tracker_rows(s, e), ob.tracker(e).rows(),
+                                              err_msg=f"tracker env {e} step {k}")
+    assert n_done >= 2 * E   # every env auto-reset at least twice after the restore
+    b.close()
+
+
 def test_checkpoint_refuses_other_configuration():
     mg = _mg()
     a = mg.BatchedEnv(grid("map1.txt"), 16, 5, 50, 100, seed=1)

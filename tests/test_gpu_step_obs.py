@@ -67,6 +67,7 @@ def test_step_obs_subset_outputs_and_oracle():
     for k in range(60):
         ints = rs.randint(0, 15, size=(E, A)).astype(np.uint8)
         r, sh, d, obs = env.step_obs(torch.from_numpy(ints).cuda(), which=("actor_vec", "critic_vec"))
+        assert obs["actor_map"] is None and obs["critic_map"] is None   # not written: not returned
         r0, s0, d0 = ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS)
         assert np.array_equal(r.cpu().numpy(), r0) and np.array_equal(sh.cpu().numpy(), s0), k
         assert np.array_equal(d.cpu().numpy().astype(bool), d0), k

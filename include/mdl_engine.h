@@ -179,6 +179,16 @@ int mdl_mail_reset(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream);
 /* The rows of those envs only (after other engine calls on `stream`). */
 int mdl_mail_export(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream);
 
+/* Host-mapped scratch for the helper-compatible calls on single dicts (convert_observation,
+ * generate_vector_features, convert_global_state, compute_shaped_rewards: MAPPO/helper.py:6-369):
+ * the caller packs the view records into it and passes its addresses to mdl_views_* as both the
+ * inputs and the outputs -- the kernels read and write host memory directly -- then calls
+ * mdl_host_wait, which returns once everything queued on `stream` before it has finished (a
+ * one-wave kernel publishes a completion word the call spins on).  mdl_host_arena returns at least
+ * `bytes` of it (16-byte aligned; a larger request replaces the arena, so earlier addresses die). */
+int mdl_host_arena(MdlEngine* eng, int64_t bytes, void** out);
+int mdl_host_wait(MdlEngine* eng, void* stream);
+
 /* ---- checkpoint of the engine state ----
  * A versioned host blob: a 56-byte header (magic "MDLSTATE", version, E, A, P, T, tracker mode,
  * map fingerprint) then every state buffer (robots, packages, state words, env records,

@@ -136,6 +136,10 @@ struct MdlEngine {
     unsigned mail_waves = 0;           // host mirror of *mail_ctr once the last export ended
     int32_t mail_seq = 0;              // last completion value published
     std::vector<uint8_t> mail_seen;    // duplicate-id check of a call
+    // host-mapped arena of the helper-compatible calls (mdl_host_arena / mdl_host_wait)
+    void* arena = nullptr;
+    size_t arena_bytes = 0;
+    int32_t arena_seq = 0;
 
     // (device pointer, bytes) of every state buffer, in checkpoint order
     // (the greedy agents' records follow when with_greedy: they exist once mdl_greedy_init ran)
@@ -170,6 +174,7 @@ struct MdlEngine {
     ~MdlEngine() {
         for (void* v : allocs) (void)hipFree(v);
         if (mail) (void)hipHostFree(mail);
+        if (arena) (void)hipHostFree(arena);
     }
 };
 
@@ -418,8 +423,8 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) eng->n_cu = prop.multiProcessorCount;
     }
     p.obs_plane_words = mdl::obs_plane_words((int)A, eng->maxHW);
-    p.obs_small = mdl::obs_use_small((int)A, (int)P, p.key7_dsh, eng->maxHW) && !getenv("MDL_OBS_GENERIC");
-    eng->lds_obs = p.obs_small ? mdl::obs_lds_small((int)A, eng->maxHW)
+    p.obs_small = mdl::obs_use_small((int)A, (int)P, p.key7_dsh, eng->maxHW, p.MO, p.MP) && !getenv("MDL_OBS_GENERIC");
+    eng->lds_obs = p.obs_small ? mdl::obs_lds_small((int)A, eng->maxHW, (int)P, p.MO, p.MP)
                                : mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MO, p.MP, p.MR, p.MPs);
     eng->wpb_obs = waves_per_block(eng->lds_obs);
     if (const char* v = getenv("MDL_OBS_WPB")) {   // profiling override (1..4 waves per workgroup)
@@ -598,6 +603,22 @@ int mail_check_ids(MdlEngine* eng, int32_t n, int32_t use_ids, const char* who) 
     return rc;
 }
 
+// Spin until the device publishes `want` in the host-mapped word `seq` (written last, with a
+// system-scope release, by the final kernel of the call): no stream synchronisation, whose
+// wake-up costs microseconds more.  A failed launch never publishes, so the stream is asked now
+// and then.
+int spin_wait(volatile const int32_t* seq, int32_t want, hipStream_t s, const char* who) {
+    for (unsigned long spins = 1;; spins++) {
+        if (*seq == want) return 0;
+        __builtin_ia32_pause();
+        if ((spins & 0xffff) == 0) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q != hipSuccess && q != hipErrorNotReady) return fail("%s: %s", who, hipGetErrorString(q));
+            if (q == hipSuccess && *seq != want) return fail("%s: the call finished without publishing", who);
+        }
+    }
+}
+
 // export the call's rows into the mailbox, then wait (spinning) for the completion word
 int mail_finish(MdlEngine* eng, int32_t n, int32_t use_ids, hipStream_t s, const char* who) {
     const MdlMailbox& m = eng->mbox;
@@ -606,17 +627,7 @@ int mail_finish(MdlEngine* eng, int32_t n, int32_t use_ids, hipStream_t s, const
     const unsigned base = eng->mail_waves;
     eng->mail_waves += mdl::mail_export_waves(n);   // the device counter's value after this launch
     HIPCHK(mdl::launch_mail_export(eng->p, use_ids ? m.ids : nullptr, n, rows, eng->mail_ctr, base, want, s));
-    volatile const int32_t* seq = m.seq;
-    for (unsigned long spins = 1;; spins++) {
-        if (*seq == want) break;
-        __builtin_ia32_pause();
-        if ((spins & 0xffff) == 0) {   // a failed launch never publishes: ask the stream now and then
-            const hipError_t q = hipStreamQuery(s);
-            if (q != hipSuccess && q != hipErrorNotReady) return fail("%s: %s", who, hipGetErrorString(q));
-            if (q == hipSuccess && *seq != want) return fail("%s: the export finished without publishing", who);
-        }
-    }
-    return 0;
+    return spin_wait(m.seq, want, s, who);
 }
 }  // namespace
 
@@ -642,6 +653,38 @@ int mdl_mail_reset(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(mdl::launch_reset(eng->p, use_ids ? eng->mbox.ids : nullptr, n, eng->wpb_step, eng->lds_step, s));
     return mail_finish(eng, n, use_ids, s, "mdl_mail_reset");
+}
+
+int mdl_host_arena(MdlEngine* eng, int64_t bytes, void** out) {
+    if (!eng || !out || bytes < 0) return fail("mdl_host_arena: bad argument");
+    if (!eng->arena || (size_t)bytes > eng->arena_bytes) {
+        size_t cap = 64 * 1024;
+        while (cap < (size_t)bytes) cap *= 2;
+        DeviceGuard dg(eng->device);
+        if (eng->arena) {   // every call on it has returned (the waits are synchronous)
+            (void)hipHostFree(eng->arena);
+            eng->arena = nullptr;
+        }
+        void* a = nullptr;
+        HIPCHK(hipHostMalloc(&a, cap + 256, hipHostMallocCoherent | hipHostMallocMapped));
+        memset(a, 0, 256);
+        eng->arena = a;
+        eng->arena_bytes = cap;
+        eng->arena_seq = 0;
+    }
+    *out = (char*)eng->arena + 256;   // the first 256 bytes hold the completion word
+    return 0;
+}
+
+int mdl_host_wait(MdlEngine* eng, void* stream) {
+    if (!eng) return fail("mdl_host_wait: null engine");
+    if (!eng->arena) return fail("mdl_host_wait: call mdl_host_arena first");
+    DeviceGuard dg(eng->device);
+    hipStream_t s = (hipStream_t)stream;
+    int32_t* seq = (int32_t*)eng->arena;
+    const int32_t want = eng->arena_seq = (eng->arena_seq % 0x7ffffff0) + 1;
+    HIPCHK(mdl::launch_publish(seq, want, s));
+    return spin_wait(seq, want, s, "mdl_host_wait");
 }
 
 int mdl_mail_export(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream) {

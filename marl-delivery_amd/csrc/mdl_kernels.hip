@@ -1487,8 +1487,19 @@ __global__ __launch_bounds__(256) void k_mail_export(DevParams p, const int32_t*
     }
 }
 
+// one wave: publish `seq` (host-mapped) once every kernel queued before it on the stream has
+// ended (their stores are released at their ends) -- mdl_host_wait's completion word
+__global__ __launch_bounds__(64) void k_publish(int32_t* seq, int32_t value) {
+    if (threadIdx.x == 0) __hip_atomic_store(seq, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------- launchers
 static int blocks_for(int n, int wpb) { return (n + wpb - 1) / wpb; }
+
+hipError_t launch_publish(int32_t* seq, int32_t value, hipStream_t s) {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, seq, value);
+    return hipGetLastError();
+}
 
 unsigned mail_export_waves(int n) { return 4u * (unsigned)blocks_for(n > 0 ? n : 1, 4); }
 
@@ -1709,9 +1720,9 @@ hipError_t launch_export(const DevParams& p, int32_t* robots, int32_t* pkgs, int
 }
 
 size_t step_lds(int P) { return reset_lds_bytes(P); }
-size_t obs_lds_small(int A, int HW) { return obs_small_lds(A, HW); }
-bool obs_use_small(int A, int P, int key7_dsh, int maxHW) {
-    return obs_small_ok(A, P, key7_dsh, maxHW);
+size_t obs_lds_small(int A, int HW, int P, int MO, int MP) { return obs_small_lds(A, HW, P, MO, MP); }
+bool obs_use_small(int A, int P, int key7_dsh, int maxHW, int MO, int MP) {
+    return obs_small_ok(A, P, key7_dsh, maxHW, MO, MP);
 }
 size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs) {
     const int MPc = MP < P ? MP : P, MPsc = MPs < P ? MPs : P;

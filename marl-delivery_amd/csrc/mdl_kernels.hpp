@@ -41,6 +41,7 @@ struct MailRows {
     double* total;     // [E]
     int32_t* rterms;   // [E] RT_* bits
 };
+hipError_t launch_publish(int32_t* seq, int32_t value, hipStream_t s);
 unsigned mail_export_waves(int n);   // waves of one k_mail_export launch over n envs
 hipError_t launch_mail_export(const DevParams& p, const int32_t* ids, int n, const MailRows& m, unsigned* ctr,
                               unsigned base, int32_t seq, hipStream_t s);
@@ -73,8 +74,8 @@ size_t views_alt_lds(int NSmax, int HW);
 size_t step_lds(int P);
 size_t obs_lds(int A, int P, int HW, int MO, int MP, int MR, int MPs);
 int obs_plane_words(int A, int HW);
-size_t obs_lds_small(int A, int HW);
-bool obs_use_small(int A, int P, int key7_dsh, int maxHW);
+size_t obs_lds_small(int A, int HW, int P, int MO, int MP);
+bool obs_use_small(int A, int P, int key7_dsh, int maxHW, int MO, int MP);
 size_t views_lds(int NSmax, int HW, int MO, int MPc, int MR, int MPsc);
 size_t views_shaped_lds(int NSmax);
 

@@ -26,6 +26,14 @@
 #ifndef MDL_OBS_EARLYFILL
 #define MDL_OBS_EARLYFILL 1
 #endif
+// Single-write actor vectors (mostly-padding vectors, e.g. the 1007-dim one): the tuples are
+// assembled in an LDS image of each agent's data slots and the env's whole actor-vector slab
+// is then streamed once as aligned float4s -- data float4s from the image, padding float4s as
+// zeros -- instead of a zero-filled slab overwritten by the tuples after a vmcnt(0) wait
+// (which wrote the tuple bytes twice).  Replaces the early fill when it applies.
+#ifndef MDL_OBS_SINGLEWRITE
+#define MDL_OBS_SINGLEWRITE 1
+#endif
 
 namespace mdl {
 
@@ -185,15 +193,28 @@ __device__ inline uint32_t sort64_u32(uint32_t x) {
 // image (6A NW words), the critic planes' (4 NW words), carrier table and critic
 // order (64 words each), order -> slot map (128 B), package order of each agent
 // (8 x 64 B), each agent's (cell, carried target) index (16 words).
-__host__ __device__ inline size_t obs_small_lds(int A, int HW) {
+__host__ __device__ inline size_t obs_small_lds_base(int A, int HW) {
     const int NW = (HW + 31) / 32;
-    return 4 * (size_t)((6 * A + 9) * NW + 1) + 2 * 256 + 128 + 512 + 64;
+    return (4 * (size_t)((6 * A + 9) * NW + 1) + 2 * 256 + 128 + 512 + 64 + 15) & ~(size_t)15;
+}
+// Floats per agent of the single-write image: self + MOc other-robot tuples, then MPc package slots.
+__host__ __device__ inline int obs_sw_stride(int MOc, int MPc) { return 6 + 5 * MOc + 5 * MPc; }
+// Whether the single-write path applies to this configuration (the device also needs a 16-B
+// aligned output, else it takes the early-fill path, which fits the same LDS slice).
+__host__ __device__ inline bool obs_sw_config(int A, int P, int MO, int MP) {
+    const int MOc = MO < A - 1 ? MO : A - 1, MPc = MP < P ? MP : P;
+    return MDL_OBS_SINGLEWRITE && (MO > MOc || MP > MPc);
+}
+__host__ __device__ inline size_t obs_small_lds(int A, int HW, int P, int MO, int MP) {
+    const int MOc = MO < A - 1 ? MO : A - 1, MPc = MP < P ? MP : P;
+    const size_t img = obs_sw_config(A, P, MO, MP) ? 4 * (((size_t)A * obs_sw_stride(MOc, MPc) + 3) & ~(size_t)3) : 0;
+    return obs_small_lds_base(A, HW) + img;
 }
 
 // Eligibility (host and device agree): A <= 8 robots, P <= 64 packages, the
 // package sort key (max(0,dl-t), rank, 7-bit order) in 32 bits, LDS slice <= 16 KiB.
-__host__ __device__ inline bool obs_small_ok(int A, int P, int key7_dsh, int maxHW) {
-    return A >= 1 && A <= 8 && P >= 1 && P <= WAVE && key7_dsh > 0 && obs_small_lds(A, maxHW) <= 16384;
+__host__ __device__ inline bool obs_small_ok(int A, int P, int key7_dsh, int maxHW, int MO, int MP) {
+    return A >= 1 && A <= 8 && P >= 1 && P <= WAVE && key7_dsh > 0 && obs_small_lds(A, maxHW, P, MO, MP) <= 16384;
 }
 
 // The builder's body for env e (output row w) from its state words as the lanes hold
@@ -242,7 +263,8 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
     // as one contiguous float4 stream, and the filled tuples are written over it
     // later, after an s_waitcnt vmcnt(0) (stores count in vmcnt on gfx9: the
     // zeros have reached L2 before any overwrite is issued).
-    const bool av_early = (MDL_OBS_EARLYFILL & 1) && avec && (MO > MOc || MP > MPc);
+    const bool sw = avec && obs_sw_config(A, P, MO, MP) && (((uintptr_t)avec & 15) == 0);
+    const bool av_early = !sw && (MDL_OBS_EARLYFILL & 1) && avec && (MO > MOc || MP > MPc);
     const bool cv_early = (MDL_OBS_EARLYFILL & 2) && cvec && (MR > A || MPs > P);
     if (av_early) zero_fill(avec + (size_t)w * A * (6 + 5 * MO + 5 * MP + 1), A * (6 + 5 * MO + 5 * MP + 1));
     if (cv_early) zero_fill(cvec + (size_t)w * (6 * MR + 7 * MPs + 1), 6 * MR + 7 * MPs + 1);
@@ -387,8 +409,17 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
         const int nq_o = A * A, ns = nq_o + A * MPc + A <= WAVE ? MPc : want;
         const int nq_p = A * ns, ntup = nq_o + nq_p + A;
         const float inv_a = 1.0f / (float)A, inv_w = ns > 0 ? 1.0f / (float)ns : 0.0f;
+        // single-write: agent a's data slots in the LDS image at img + a * L (zeroed first)
+        const int L = obs_sw_stride(MOc, MPc);
+        float* img = (float*)(smem_wave + obs_small_lds_base(A, HW));
+        if (sw) {
+            const int nz = (A * L + 3) >> 2;
+            for (int q = lane; q < nz; q += WAVE) reinterpret_cast<float4*>(img)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
         wave_sync();
+#ifndef MDL_EXP_NOWAIT   // profiling builds only (wrong results): no wait between the fill and the tuples
         if (av_early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slab's zeros are in L2
+#endif
         for (int q0 = 0; q0 < ntup; q0 += WAVE) {   // uniform trip count
             const int q = q0 + lane;
             const bool is_o = q < nq_o, is_p = !is_o && q < nq_o + nq_p, is_s = !is_o && !is_p && q < ntup;
@@ -436,9 +467,13 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
             const float d1 = qdiv_r(x1, yH), d2 = qdiv_r(x2, yW), d3 = qdiv_r(x3, yH), d4 = qdiv_r(x4, yW);
             const float d5 = qdiv_r(x5, yT);   // x5 = 0 when T <= 0
             const float fl = o_cy != 0 ? 1.0f : 0.0f;
+#ifdef MDL_EXP_NOTUPLES   // profiling builds only (wrong results): the actor vectors' tuples are not stored
+            if (false) {
+#else
             if ((ovalid && opos < MO) || is_p || is_s) {
-                const int off = qa * Dv + (is_s ? 0 : is_o ? 6 + 5 * opos : 6 + 5 * MO + 5 * qb);
-                float* o = av + off;
+#endif
+                const int off = is_s ? 0 : is_o ? 6 + 5 * opos : 6 + 5 * (sw ? MOc : MO) + 5 * qb;
+                float* o = sw ? img + qa * L + off : av + qa * Dv + off;
                 o[0] = d1;
                 o[1] = d2;
                 o[2] = is_p ? d3 : fl;
@@ -446,12 +481,68 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
                 o[4] = is_p ? d5 : d4;
                 if (is_s) {
                     o[5] = d5;
-                    o[Dv - 1] = qdiv_r(t, yT);   // yT = 0 when T <= 0
+                    if (!sw) o[Dv - 1] = qdiv_r(t, yT);   // yT = 0 when T <= 0
                 }
             }
         }
+        if (sw) {
+            // Stream the env's slab [g0, g0 + A*Dv) (floats from avec, 16-B aligned) once: the
+            // float4 covers of the data intervals -- X(a) = [a*Dv - 1, a*Dv + 6 + 5MOc) (the
+            // previous agent's t/T, self, filled other-robot slots), Pk(a) = [a*Dv + 6 + 5MO,
+            // +5*want) (filled package slots), the last agent's t/T -- from the image, every
+            // float4 between them as zeros.  Covers of neighbouring intervals may share a float4:
+            // both passes write the same complete value.  Only the slab's first / last float4 can
+            // hold another env's floats: those are written per float.
+            wave_sync();
+            const float tval = qdiv_r(t, yT);
+            const int g0 = w * A * Dv, S = A * Dv;
+            const int xe = 6 + 5 * MOc, ps0 = 6 + 5 * MO, pe = 5 * MPc;
+            float4* a4 = reinterpret_cast<float4*>(avec);
+            auto value = [&](int a, int o) -> float {   // float o of agent a's vector (o in [-4, Dv + 4))
+                const bool neg = o < 0;
+                const int aa = neg ? a - 1 : a, oo = neg ? o + Dv : o;
+                const bool inx = aa >= 0 && oo < xe, inp = aa >= 0 && (unsigned)(oo - ps0) < (unsigned)pe;
+                const float v = (inx || inp) ? img[aa * L + (inx ? oo : oo - (ps0 - xe))] : 0.0f;
+                return oo == Dv - 1 ? tval : v;
+            };
+            int qprev = g0 >> 2;   // end (float4 index) of the previous cover
+            for (int k = 0; k <= 2 * A; k++) {   // X(0), Pk(0), X(1), ..., Pk(A-1), then the last t/T
+                const int a = k >> 1;
+                int s0, s1;
+                if (k == 2 * A) {
+                    s0 = S - 1;
+                    s1 = S;
+                } else if (k & 1) {
+                    s0 = a * Dv + ps0;
+                    s1 = s0 + 5 * want;
+                } else {
+                    s0 = a * Dv - (a > 0 ? 1 : 0);
+                    s1 = a * Dv + xe;
+                }
+                if (s1 <= s0) continue;
+                const int qs = (g0 + s0) >> 2, qe = (g0 + s1 + 3) >> 2;
+                for (int q = qprev + lane; q < qs; q += WAVE) a4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                const int ab = k == 2 * A ? A - 1 : a;   // the agent the offsets below are relative to
+                for (int q = qs + lane; q < qe; q += WAVE) {
+                    const int f0 = 4 * q - g0;            // slab-relative index of the float4's first float
+                    const int o0 = f0 - ab * Dv;
+                    const float v0 = value(ab, o0), v1 = value(ab, o0 + 1), v2 = value(ab, o0 + 2),
+                                v3 = value(ab, o0 + 3);
+                    if (f0 >= 0 && f0 + 4 <= S) {
+                        a4[q] = make_float4(v0, v1, v2, v3);
+                    } else {
+                        float* d = avec + 4 * (size_t)q;
+                        if ((unsigned)f0 < (unsigned)S) d[0] = v0;
+                        if ((unsigned)(f0 + 1) < (unsigned)S) d[1] = v1;
+                        if ((unsigned)(f0 + 2) < (unsigned)S) d[2] = v2;
+                        if ((unsigned)(f0 + 3) < (unsigned)S) d[3] = v3;
+                    }
+                }
+                qprev = qe > qprev ? qe : qprev;
+            }
+        }
         // padding: other-robot slots [MOc, MO) and package slots [ns, MP) of every agent
-        if (!av_early && (MO > MOc || MP > ns)) {
+        if (!sw && !av_early && (MO > MOc || MP > ns)) {
             for (int a = 0; a < A; a++) {
                 zero_fill(av + a * Dv + 6 + 5 * MOc, 5 * (MO - MOc));
                 zero_fill(av + a * Dv + 6 + 5 * MO + 5 * ns, 5 * (MP - ns));

@@ -75,6 +75,8 @@ SIGNATURES = {
     "mdl_mail_step": (C.c_int, [_vp, _i32, _i32, _i32, _vp]),
     "mdl_mail_reset": (C.c_int, [_vp, _i32, _i32, _vp]),
     "mdl_mail_export": (C.c_int, [_vp, _i32, _i32, _vp]),
+    "mdl_host_arena": (C.c_int, [_vp, C.c_int64, C.POINTER(C.c_void_p)]),
+    "mdl_host_wait": (C.c_int, [_vp, _vp]),
     "mdl_state_bytes": (C.c_int, [_vp, C.POINTER(C.c_int64)]),
     "mdl_save_state": (C.c_int, [_vp, _vp, C.c_int64, _vp]),
     "mdl_load_state": (C.c_int, [_vp, _vp, C.c_int64, _vp]),

@@ -10,43 +10,49 @@ the batched form over an engine's envs is ``BatchedEnv.build_obs_alt``.
 """
 from __future__ import annotations
 
-import ctypes as C
-
 import numpy as np
 
-from ._lib import check, lib, stream_handle
-from .helper import _engine_for, _layout, _tracker_rows, _xfer, pack_view
+from . import _mdl_pack
+from ._lib import check, lib
+from ._lib import raw_stream as _raw_stream
+from .helper import _align, _arena, _engine_for, _tracker_rows
 
 OP_NO_MATCH = 255   # a string op: the reference compares it with the ints 1 / 2 and never matches
 
 
 def _alt(state, persistent_packages, agent_indices, shape, want):
-    """One upload (views, offsets, agent indices), the kernel, one download -> numpy."""
+    """The view record packed into the engine's host-mapped arena, the kernel reading it there
+    and writing its outputs there, one completion wait -> numpy (as marl_gpu.helper.features)."""
     grid = state["map"]
     eng = _engine_for(grid)
     H, W = len(grid), len(grid[0])
-    rows = _tracker_rows(persistent_packages)
-    view = pack_view(state["time_step"], state["robots"], rows, H, W)
+    robots = state["robots"]
+    ns = len(persistent_packages)
     n = len(agent_indices)
-    x = _xfer(eng)
-    (o_v, o_o, o_i), nin = _layout([(view.size * n, 1), (2 * n, 2), (n, 1)])
-    words = np.zeros(nin, np.int32)
-    words[o_v:o_v + view.size * n] = np.tile(view, n)
-    words[o_o:o_o + 2 * n] = (np.arange(n, dtype=np.int64) * view.size).view(np.int32)
-    words[o_i:o_i + n] = np.asarray(agent_indices, np.int32)
-    b = x.up(words).data_ptr()
+    vw = 4 + 3 * len(robots) + 8 * ns
     oh, ow = (shape[1], shape[2]) if shape is not None else (H, W)
     names = [k for k in ("idq", "qmix") if k in want]
     sizes = {"idq": 6 * H * W, "qmix": 7 * oh * ow}
-    offs, nout = _layout([(n * sizes[k], 4) for k in names])
-    dout = x.out(nout)
-    ptrs = {k: dout.data_ptr() + 4 * o for k, o in zip(names, offs)}
-    check(lib().mdl_views_alt_features(eng._h, b + 4 * o_v, b + 4 * o_o, n, int(rows.shape[0]), b + 4 * o_i,
-                                       ptrs.get("idq"), ptrs.get("qmix"), int(oh), int(ow),
-                                       C.c_void_p(stream_handle())), "mdl_views_alt_features")
-    host = x.down(nout)
+    o_off = _align(4 * vw)
+    o_idx = _align(o_off + 8 * n)
+    pos = _align(o_idx + 4 * n)
+    o_out = {}
+    for k in names:
+        o_out[k] = pos
+        pos = _align(pos + 4 * n * sizes[k])
+    ar = _arena(eng)
+    u8 = ar.get(pos)
+    b = ar.addr
+    _mdl_pack.pack_view(b, vw, int(state["time_step"]), robots, persistent_packages, H, W, 0)
+    u8[o_off:o_off + 8 * n] = 0
+    u8[o_idx:o_idx + 4 * n].view(np.int32)[:] = agent_indices
+    check(lib().mdl_views_alt_features(eng._h, b, b + o_off, n, ns, b + o_idx,
+                                       b + o_out["idq"] if "idq" in o_out else None,
+                                       b + o_out["qmix"] if "qmix" in o_out else None, int(oh), int(ow),
+                                       _raw_stream(ar._dev)), "mdl_views_alt_features")
+    ar.wait()
     shapes = {"idq": (n, 6, H, W), "qmix": (n, 7, oh, ow)}
-    res = {k: host[o:o + n * sizes[k]].reshape(shapes[k]) for k, o in zip(names, offs)}
+    res = {k: u8[o_out[k]:o_out[k] + 4 * n * sizes[k]].view(np.float32).reshape(shapes[k]).copy() for k in names}
     return res.get("idq"), res.get("qmix")
 
 
@@ -73,38 +79,35 @@ def reward_shaping(prev_env_state, current_env_state, actions_taken, persistent_
     cur_r = list(current_env_state["robots"])[:num_agents]
     t_cur = int(current_env_state["time_step"])
     t_prev = int(prev_env_state.get("time_step", t_cur - 1))
-    H = max([r[0] for r in prev_r + cur_r] + [1])
-    W = max([r[1] for r in prev_r + cur_r] + [1])
-    rows = _tracker_rows(persistent_packages_before_action)
-    if rows.size:
-        H = max(H, int(rows[:, [2, 4]].max()) + 1)
-        W = max(W, int(rows[:, [3, 5]].max()) + 1)
     grid = prev_env_state.get("map")
-    if grid is None:
+    if grid is None:   # a map large enough for every coordinate used
+        H = max([r[0] for r in prev_r + cur_r] + [1])
+        W = max([r[1] for r in prev_r + cur_r] + [1])
+        rows = _tracker_rows(persistent_packages_before_action)
+        if rows.size:
+            H = max(H, int(rows[:, [2, 4]].max()) + 1)
+            W = max(W, int(rows[:, [3, 5]].max()) + 1)
         grid = np.zeros((H, W), np.uint8)
     eng = _engine_for(grid)
     Hm, Wm = len(grid), len(grid[0])
-    prev = pack_view(t_prev, prev_r, rows, Hm, Wm)
-    cr = np.asarray(cur_r, np.int64).reshape(-1, 3).copy()
-    cr[:, :2] -= 1
-    cur = np.concatenate([[t_cur, cr.shape[0]], cr.reshape(-1)]).astype(np.int32)
-    ops = np.array([int(a[1]) if isinstance(a[1], (int, np.integer)) and not isinstance(a[1], bool)
-                    and 0 <= int(a[1]) < 255 else OP_NO_MATCH for a in actions_taken[:num_agents]], np.uint8)
-    x = _xfer(eng)
-    ow_ = (ops.size + 3) // 4
-    (o_p, o_c, o_a, o_off), nin = _layout([(prev.size, 1), (cur.size, 1), (ow_, 1), (6, 2)])
-    words = np.zeros(nin, np.int32)
-    words[o_p:o_p + prev.size] = prev
-    words[o_c:o_c + cur.size] = cur
-    ab = np.zeros(4 * ow_, np.uint8)
-    ab[:ops.size] = ops
-    words[o_a:o_a + ow_] = ab.view(np.int32)
-    b = x.up(words).data_ptr()
-    out = x.out(2 * num_agents + 2)
-    o64 = (out.data_ptr() + 7) // 8 * 8   # f64 outputs, 8-B aligned in the float buffer
-    check(lib().mdl_views_idq_reward(eng._h, b + 4 * o_p, b + 4 * o_off, int(rows.shape[0]), b + 4 * o_c,
-                                     b + 4 * o_off, b + 4 * o_a, b + 4 * o_off, 1, 1, o64,
-                                     C.c_void_p(stream_handle())), "mdl_views_idq_reward")
-    host = x.down(2 * num_agents + 2)
-    sh = (o64 - out.data_ptr()) // 4
-    return [float(v) for v in host[sh:sh + 2 * num_agents].view(np.float64)]
+    ops = bytes(int(a[1]) if isinstance(a[1], (int, np.integer)) and not isinstance(a[1], bool)
+                and 0 <= int(a[1]) < 255 else OP_NO_MATCH for a in actions_taken[:num_agents])
+    ns = len(persistent_packages_before_action)
+    vw = 4 + 3 * len(prev_r) + 8 * ns
+    cw = 2 + 3 * len(cur_r)
+    # arena: prev view | cur record | op bytes | three int64 offsets (0) | out (f64 per agent)
+    o_c = _align(4 * vw)
+    o_a = _align(o_c + 4 * cw)
+    o_off = _align(o_a + len(ops))
+    o_out = o_off + 32
+    ar = _arena(eng)
+    u8 = ar.get(o_out + 8 * max(1, num_agents) + 16)
+    b = ar.addr
+    _mdl_pack.pack_view(b, vw, t_prev, prev_r, persistent_packages_before_action, Hm, Wm, 0)
+    _mdl_pack.pack_robots(b + o_c, cw, t_cur, cur_r)
+    u8[o_a:o_a + len(ops)] = np.frombuffer(ops, np.uint8)
+    u8[o_off:o_off + 32] = 0
+    check(lib().mdl_views_idq_reward(eng._h, b, b + o_off, ns, b + o_c, b + o_off, b + o_a, b + o_off, 1, 1,
+                                     b + o_out, _raw_stream(ar._dev)), "mdl_views_idq_reward")
+    ar.wait()
+    return [float(v) for v in u8[o_out:o_out + 8 * num_agents].view(np.float64)]

@@ -9,19 +9,24 @@ generate_vector_features):
   convert_global_state(state, tracker, T, MR=100, MPs=100)         -> (f32[4,H,W], f32[Dg])  :167-255
   compute_shaped_rewards(g, prev, cur, actions, tracker_prev, A)   -> np.float32   :257-369
 
-Each call packs the dict(s) into the engine's view record format, uploads it,
-and runs the same device code the batched engine uses (mdl_views_features /
-mdl_views_shaped_reward).  They exist for drop-in use and for the known-answer
-tests; batched training should use BatchedEnv.build_obs instead.
+Each call packs the dict(s) into the engine's view record format straight into
+the engine's host-mapped arena (a C extension walks the dicts: _mdl_pack), runs
+the same device code the batched engine uses (mdl_views_features /
+mdl_views_shaped_reward) reading its inputs from and writing its outputs to
+that host memory, and waits for a completion word (mdl_host_wait): one kernel
+launch plus a one-wave publish, no copies and no stream synchronisation.
+They exist for drop-in use and for the known-answer tests; batched training
+should use BatchedEnv.build_obs instead.
 """
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
-import torch
 
-from ._lib import check, lib, stream_handle
+from . import _mdl_pack
+from ._lib import check, lib
+from ._lib import raw_stream as _raw_stream
 from .engine import MAPPO_SHAPING, QMIX_SHAPING, BatchedEnv
 from .compat import MOVE_CODES, OP_CODES
 
@@ -38,6 +43,43 @@ def _engine_for(grid) -> BatchedEnv:
     return eng
 
 
+class _Arena:
+    """The engine's host-mapped arena (mdl_host_arena) as one numpy byte view; grows on demand
+    (every call has finished with it on return: mdl_host_wait is synchronous)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.cap = 0
+        self.addr = 0
+        self.u8 = None
+        L = lib()
+        self._views, self._shaped, self._wait = L.mdl_views_features, L.mdl_views_shaped_reward, L.mdl_host_wait
+        self._dev = eng.device.index
+
+    def get(self, nbytes):
+        if nbytes > self.cap:
+            p = C.c_void_p()
+            check(lib().mdl_host_arena(self.eng._h, int(nbytes), C.byref(p)), "mdl_host_arena")
+            cap = 64 * 1024
+            while cap < nbytes:
+                cap *= 2
+            self.cap, self.addr = cap, p.value
+            self.u8 = np.ctypeslib.as_array((C.c_uint8 * cap).from_address(p.value))
+        return self.u8
+
+    def wait(self):
+        rc = self._wait(self.eng._h, _raw_stream(self._dev))
+        if rc:
+            check(rc, "mdl_host_wait")
+
+
+def _arena(eng) -> _Arena:
+    a = eng.__dict__.get("_arena")
+    if a is None:
+        a = eng._arena = _Arena(eng)
+    return a
+
+
 def _tracker_rows(tracker: dict) -> np.ndarray:
     rows = np.zeros((len(tracker), 8), np.int32)
     for k, v in enumerate(tracker.values()):
@@ -48,155 +90,108 @@ def _tracker_rows(tracker: dict) -> np.ndarray:
 
 def pack_view(t, robots1, tracker_rows, H, W, map_index=0) -> np.ndarray:
     """[t, A, n, map] + A*(r, c, carry) (0-indexed) + n*(id, status, sr, sc, tr, tc, st, dl)."""
-    rb = np.asarray(robots1, dtype=np.int64).reshape(-1, 3).copy()
-    rb[:, :2] -= 1
-    rows = np.asarray(tracker_rows, dtype=np.int64).reshape(-1, 8)
-    if rb.shape[0] > 64:
-        raise ValueError("at most 64 robots per view")
-    if ((rb[:, 0] < 0) | (rb[:, 0] >= H) | (rb[:, 1] < 0) | (rb[:, 1] >= W)).any():
-        raise ValueError("robot positions must lie inside the map")
-    if rows.size and ((rows[:, 2] < 0) | (rows[:, 2] >= H) | (rows[:, 4] < 0) | (rows[:, 4] >= H) |
-                      (rows[:, 3] < 0) | (rows[:, 3] >= W) | (rows[:, 5] < 0) | (rows[:, 5] >= W)).any():
-        raise ValueError("package cells must lie inside the map")
-    if rows.size and ((rows[:, 6] < 0) | (rows[:, 6] > 65535) | (rows[:, 7] < 0) | (rows[:, 7] > 65535)).any():
-        raise ValueError("start_time / deadline must fit 16 bits")
-    head = np.array([t, rb.shape[0], rows.shape[0], map_index], np.int64)
-    return np.concatenate([head, rb.reshape(-1), rows.reshape(-1)]).astype(np.int32)
+    rows = tracker_rows if isinstance(tracker_rows, dict) else np.asarray(tracker_rows, np.int64).reshape(-1, 8).tolist()
+    n = 4 + 3 * len(robots1) + 8 * len(rows)
+    out = np.zeros(n, np.int32)
+    _mdl_pack.pack_view(out.ctypes.data, n, int(t), robots1, rows, H, W, map_index)
+    return out
 
 
-class _Xfer:
-    """Pinned staging of one helper call: the packed inputs go up in ONE host-to-device copy
-    and every output comes back in ONE device-to-host copy, with one synchronisation (the
-    buffers grow on demand and are reused: each call has retired its transfers on return)."""
-
-    def __init__(self, device):
-        self.device = device
-        self.h_in = self.d_in = self.d_out = self.h_out = None
-
-    @staticmethod
-    def _grow(n):
-        return 1 << max(10, (int(n) - 1).bit_length())
-
-    def up(self, words: np.ndarray) -> torch.Tensor:
-        n = words.size
-        if self.h_in is None or self.h_in.numel() < n:
-            m = self._grow(n)
-            self.h_in = torch.empty(m, dtype=torch.int32, pin_memory=True)
-            self.d_in = torch.empty(m, dtype=torch.int32, device=self.device)
-        self.h_in.numpy()[:n] = words
-        self.d_in[:n].copy_(self.h_in[:n], non_blocking=True)
-        return self.d_in
-
-    def out(self, n: int) -> torch.Tensor:
-        if self.d_out is None or self.d_out.numel() < n:
-            m = self._grow(n)
-            self.d_out = torch.empty(m, dtype=torch.float32, device=self.device)
-            self.h_out = torch.empty(m, dtype=torch.float32, pin_memory=True)
-        return self.d_out
-
-    def down(self, n: int) -> np.ndarray:
-        self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
-        return self.h_out.numpy()[:n].copy()
+def _align(x, a=16):
+    return (x + a - 1) // a * a
 
 
-def _xfer(eng) -> _Xfer:
-    x = eng.__dict__.get("_helper_xfer")
-    if x is None:
-        x = eng._helper_xfer = _Xfer(eng.device)
-    return x
-
-
-def _layout(parts):
-    """Word offsets of consecutive parts, each starting at a multiple of its alignment (words)."""
-    offs, pos = [], 0
-    for size, align in parts:
-        pos = (pos + align - 1) // align * align
-        offs.append(pos)
-        pos += size
-    return offs, pos
-
-
-def features(state, tracker_rows, agent_indices, T, MO, MP, MR, MPs, want=("obs", "vec", "gmap", "gvec")):
-    """Batched helper entry: one view per agent index (same state / tracker)."""
+def features(state, tracker, agent_indices, T, MO, MP, MR, MPs, want=("obs", "vec", "gmap", "gvec")):
+    """Batched helper entry: one view per agent index (same state / tracker: one record that
+    every view's offset points at).  ``tracker``: the reference's tracker dict (insertion order)
+    or rows (id, status 1|2, sr, sc, tr, tc, start_time, deadline)."""
     grid = state["map"]
     eng = _engine_for(grid)
     H, W = len(grid), len(grid[0])
-    view = pack_view(state["time_step"], state["robots"], tracker_rows, H, W)
+    if not isinstance(tracker, dict):
+        tracker = np.asarray(tracker, np.int64).reshape(-1, 8).tolist()
+    robots = state["robots"]
+    ns = len(tracker)
     n = len(agent_indices)
-    x = _xfer(eng)
-    # inputs: n copies of the view, their int64 offsets, the agent indices -- one upload
-    (o_v, o_o, o_i), nin = _layout([(view.size * n, 1), (2 * n, 2), (n, 1)])
-    words = np.zeros(nin, np.int32)
-    words[o_v:o_v + view.size * n] = np.tile(view, n)
-    words[o_o:o_o + 2 * n] = (np.arange(n, dtype=np.int64) * view.size).view(np.int32)
-    words[o_i:o_i + n] = np.asarray(agent_indices, np.int32)
-    din = x.up(words)
-    base_in = din.data_ptr()
-    # outputs: one float buffer, each output 16-B aligned -- one download
+    vw = 4 + 3 * len(robots) + 8 * ns
     sizes = {"obs": 6 * H * W, "vec": 6 + 5 * MO + 5 * MP + 1, "gmap": 4 * H * W, "gvec": 6 * MR + 7 * MPs + 1}
     names = [k for k in ("obs", "vec", "gmap", "gvec") if k in want]
-    offs, nout = _layout([(n * sizes[k], 4) for k in names])
-    dout = x.out(nout)
-    ptrs = {k: dout.data_ptr() + 4 * o for k, o in zip(names, offs)}
-    ns = int(np.asarray(tracker_rows).reshape(-1, 8).shape[0])
-    check(lib().mdl_views_features(eng._h, base_in + 4 * o_v, base_in + 4 * o_o, n, ns, base_in + 4 * o_i, int(T),
-                                   MO, MP, MR, MPs, ptrs.get("obs"), ptrs.get("vec"), ptrs.get("gmap"),
-                                   ptrs.get("gvec"), C.c_void_p(stream_handle())), "mdl_views_features")
-    host = x.down(nout)
+    o_off = _align(4 * vw)                      # int64 offsets (all 0: one shared record)
+    o_idx = _align(o_off + 8 * n)
+    pos = _align(o_idx + 4 * n)
+    o_out = {}
+    for k in names:
+        o_out[k] = pos
+        pos = _align(pos + 4 * n * sizes[k])
+    ar = _arena(eng)
+    u8 = ar.get(pos)
+    base = ar.addr
+    _mdl_pack.pack_view(base, vw, int(state["time_step"]), robots, tracker, H, W, 0)
+    u8[o_off:o_off + 8 * n] = 0
+    u8[o_idx:o_idx + 4 * n].view(np.int32)[:] = agent_indices
+    rc = ar._views(eng._h, base, base + o_off, n, ns, base + o_idx, int(T), MO, MP, MR, MPs,
+                   base + o_out["obs"] if "obs" in o_out else None, base + o_out["vec"] if "vec" in o_out else None,
+                   base + o_out["gmap"] if "gmap" in o_out else None, base + o_out["gvec"] if "gvec" in o_out else None,
+                   _raw_stream(ar._dev))
+    if rc:
+        check(rc, "mdl_views_features")
+    ar.wait()
     shapes = {"obs": (n, 6, H, W), "vec": (n, sizes["vec"]), "gmap": (n, 4, H, W), "gvec": (n, sizes["gvec"])}
-    return {k: host[o:o + n * sizes[k]].reshape(shapes[k]) for k, o in zip(names, offs)}
+    return {k: u8[o_out[k]:o_out[k] + 4 * n * sizes[k]].view(np.float32).reshape(shapes[k]).copy() for k in names}
 
 
 def convert_observation(env_state_dict, persistent_packages_for_env, current_robot_idx):
-    rows = _tracker_rows(persistent_packages_for_env)
-    return features(env_state_dict, rows, [current_robot_idx], 0, 0, 0, 0, 0, want=("obs",))["obs"][0]
+    return features(env_state_dict, persistent_packages_for_env, [current_robot_idx], 0, 0, 0, 0, 0,
+                    want=("obs",))["obs"][0]
 
 
 def generate_vector_features(env_state_dict, persistent_packages_for_env, current_robot_idx, max_time_steps,
                              max_other_robots_to_observe=100, max_packages_to_observe=100):
-    rows = _tracker_rows(persistent_packages_for_env)
-    return features(env_state_dict, rows, [current_robot_idx], max_time_steps, max_other_robots_to_observe,
-                    max_packages_to_observe, 0, 0, want=("vec",))["vec"][0]
+    return features(env_state_dict, persistent_packages_for_env, [current_robot_idx], max_time_steps,
+                    max_other_robots_to_observe, max_packages_to_observe, 0, 0, want=("vec",))["vec"][0]
 
 
 def convert_global_state(env_state_dict, persistent_packages_for_env, max_time_steps, max_robots_in_state=100,
                          max_packages_in_state=100):
-    rows = _tracker_rows(persistent_packages_for_env)
-    o = features(env_state_dict, rows, [0], max_time_steps, 0, 0, max_robots_in_state, max_packages_in_state,
-                 want=("gmap", "gvec"))
+    o = features(env_state_dict, persistent_packages_for_env, [0], max_time_steps, 0, 0, max_robots_in_state,
+                 max_packages_in_state, want=("gmap", "gvec"))
     return o["gmap"][0], o["gvec"][0]
 
 
-def shaped_rewards_views(g, prev_t, prev_robots1, cur_t, cur_robots1, action_codes, tracker_rows, grid,
+def shaped_rewards_views(g, prev_t, prev_robots1, cur_t, cur_robots1, action_codes, tracker, grid,
                          consts=MAPPO_SHAPING):
-    """Raw entry for compute_shaped_rewards: packed inputs, one or many transitions."""
+    """Raw entry for compute_shaped_rewards: one transition; ``tracker``: the tracker dict of the
+    previous state (insertion order) or its rows."""
     eng = _engine_for(grid)
     H, W = len(grid), len(grid[0])
-    prev = pack_view(prev_t, prev_robots1, tracker_rows, H, W)
-    cr = np.asarray(cur_robots1, np.int64).reshape(-1, 3).copy()
-    cr[:, :2] -= 1
-    cur = np.concatenate([[cur_t, cr.shape[0]], cr.reshape(-1)]).astype(np.int32)
-    codes = np.asarray(action_codes, np.uint8).reshape(-1)
-    cw = (codes.size + 3) // 4
-    x = _xfer(eng)
-    # one upload: prev view, cur view, action bytes, three int64 offsets (all 0), g (fp64)
-    (o_p, o_c, o_a, o_off, o_g), nin = _layout([(prev.size, 1), (cur.size, 1), (cw, 1), (6, 2), (2, 2)])
-    words = np.zeros(nin, np.int32)
-    words[o_p:o_p + prev.size] = prev
-    words[o_c:o_c + cur.size] = cur
-    ab = np.zeros(4 * cw, np.uint8)
-    ab[:codes.size] = codes
-    words[o_a:o_a + cw] = ab.view(np.int32)
-    words[o_g:o_g + 2] = np.array([float(g)], np.float64).view(np.int32)
-    b = x.up(words).data_ptr()
-    out = x.out(1)
-    cs = (C.c_double * 9)(*[float(v) for v in consts])
-    ns = int(np.asarray(tracker_rows).reshape(-1, 8).shape[0])
-    check(lib().mdl_views_shaped_reward(eng._h, b + 4 * o_p, b + 4 * o_off, ns, b + 4 * o_c, b + 4 * o_off,
-                                        b + 4 * o_a, b + 4 * o_off, b + 4 * o_g, 1, cs, out.data_ptr(),
-                                        C.c_void_p(stream_handle())), "mdl_views_shaped_reward")
-    return np.float32(x.down(1)[0])
+    if not isinstance(tracker, dict):
+        tracker = np.asarray(tracker, np.int64).reshape(-1, 8).tolist()
+    ns = len(tracker)
+    A = len(prev_robots1)
+    vw = 4 + 3 * A + 8 * ns
+    cw = 2 + 3 * len(cur_robots1)
+    codes = bytes(action_codes)
+    # arena: prev view | cur record | action bytes | three int64 offsets (0) | g (f64) | out (f32)
+    o_c = _align(4 * vw)
+    o_a = _align(o_c + 4 * cw)
+    o_off = _align(o_a + len(codes))
+    o_g = o_off + 16
+    o_out = o_g + 8
+    ar = _arena(eng)
+    u8 = ar.get(o_out + 16)
+    b = ar.addr
+    _mdl_pack.pack_view(b, vw, int(prev_t), prev_robots1, tracker, H, W, 0)
+    _mdl_pack.pack_robots(b + o_c, cw, int(cur_t), cur_robots1)
+    u8[o_a:o_a + len(codes)] = np.frombuffer(codes, np.uint8)
+    u8[o_off:o_off + 16] = 0
+    u8[o_g:o_g + 8].view(np.float64)[0] = float(g)
+    cs = None if consts is None else (C.c_double * 9)(*[float(v) for v in consts])
+    rc = ar._shaped(eng._h, b, b + o_off, ns, b + o_c, b + o_off, b + o_a, b + o_off, b + o_g, 1, cs, b + o_out,
+                    _raw_stream(ar._dev))
+    if rc:
+        check(rc, "mdl_views_shaped_reward")
+    ar.wait()
+    return np.float32(u8[o_out:o_out + 4].view(np.float32)[0])
 
 
 def compute_shaped_rewards(global_reward, prev_env_state_dict, current_env_state_dict, actions_taken_for_all_agents,
@@ -207,18 +202,19 @@ def compute_shaped_rewards(global_reward, prev_env_state_dict, current_env_state
     defaults to a map large enough for the coordinates used."""
     prev_r = list(prev_env_state_dict["robots"])[:num_agents]
     cur_r = list(current_env_state_dict["robots"])[:num_agents]
-    codes = np.array([MOVE_CODES.get(m, 5) | (OP_CODES.get(o, 3) << 3)
-                      for m, o in list(actions_taken_for_all_agents)[:num_agents]], np.uint8)
-    rows = _tracker_rows(persistent_packages_at_prev_state)
+    codes = bytes(MOVE_CODES.get(m, 5) | (OP_CODES.get(o, 3) << 3)
+                  for m, o in list(actions_taken_for_all_agents)[:num_agents])
+    trk = persistent_packages_at_prev_state
     if grid is None:
         grid = prev_env_state_dict.get("map")
     if grid is None:
+        rows = _tracker_rows(trk) if isinstance(trk, dict) else np.asarray(trk).reshape(-1, 8)
         coords = [x for r in prev_r + cur_r for x in r[:2]]
         coords += [int(v) + 1 for row in rows for v in row[2:6]]
         n = max(coords + [2])
         grid = [[0] * n for _ in range(n)]
     return shaped_rewards_views(global_reward, prev_env_state_dict["time_step"], prev_r,
-                                current_env_state_dict["time_step"], cur_r, codes, rows, grid, consts)
+                                current_env_state_dict["time_step"], cur_r, codes, trk, grid, consts)
 
 
 __all__ = ["convert_observation", "generate_vector_features", "convert_global_state", "compute_shaped_rewards",

@@ -15,6 +15,9 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
+MIXED_TOTAL = 23   # config 4's layout at test size: groups 5, 5, 5, 4, 4; ranks [0, 12), [12, 23)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -39,17 +42,25 @@ def _worker(rank, world, port, mode, out_q):
     base, per, total = 42, 6, 11
     if mode == "weak":
         ids, seeds = D.shard(per, r, base)
-    else:
+        runs = [(0, 0, len(ids))]
+    elif mode == "strong":
         ids, seeds = D.shard_strong(total, r, w, base)
-    g = grid("map1.txt")
+        runs = [(0, 0, len(ids))]
+    else:   # config 4: map1..map5 groups back to back, dealt to the ranks in contiguous blocks
+        ids, seeds, env_map, runs = D.shard_mixed(MIXED_TOTAL, 5, r, w, base)
+        assert [env_map[b] for _, b, _ in runs] == [m for m, _, _ in runs]
+    grids = [grid(f"map{i}.txt") for i in range(1, 6)] if mode == "mixed" else [grid("map1.txt")]
     E = len(ids)
-    ob = O.OracleBatch(E, g, 5, 20, 30, seed_base=seeds[0], clear_on_reset=False)
+    # one oracle batch per same-map run of this rank (seeds base + global id, contiguous)
+    obs = [(b, n, O.OracleBatch(n, grids[m], 5, 20, 30, seed_base=seeds[b], clear_on_reset=False))
+           for m, b, n in runs]
     rs = np.random.RandomState(3)
-    n_global = per * w if mode == "weak" else total
+    n_global = per * w if mode == "weak" else total if mode == "strong" else MIXED_TOTAL
     rewards = []
     for k in range(45):
         acts = rs.randint(0, 15, size=(n_global, 5)).astype(np.uint8)
-        rr, sh, dn = ob.step(acts[ids[0]:ids[0] + E], auto_reset=True, consts=O.MAPPO_CONSTS)
+        parts = [ob.step(acts[ids[0] + b:ids[0] + b + n], auto_reset=True, consts=O.MAPPO_CONSTS) for b, n, ob in obs]
+        rr, sh, dn = (np.concatenate([p[i] for p in parts]) for i in range(3))
         rewards.append(np.stack([rr, sh.astype(np.float64), dn.astype(np.float64)], 1))
     mine = torch.from_numpy(np.stack(rewards, 0))            # [K, E, 3]
     sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(w)]
@@ -67,8 +78,11 @@ def _worker(rank, world, port, mode, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["weak", "strong"])
+@pytest.mark.parametrize("mode", ["weak", "strong", "mixed"])
 def test_sharded_streams_equal_single_process(mode):
+    """weak / strong: config 2's map1 batch; mixed: config 4's layout (map1..map5 groups back
+    to back, 23 envs so that a rank boundary falls inside a map group) -- the sharded streams
+    equal one process running every env with seed 42 + global id."""
     import oracle as O
     from golden_io import grid
     ctx = mp.get_context("spawn")
@@ -82,12 +96,21 @@ def test_sharded_streams_equal_single_process(mode):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert t_max == [2.0, 2.0]
-    n = 12 if mode == "weak" else 11
-    ob = O.OracleBatch(n, grid("map1.txt"), 5, 20, 30, seed_base=42, clear_on_reset=False)
+    n = 12 if mode == "weak" else 11 if mode == "strong" else MIXED_TOTAL
+    if mode == "mixed":
+        from marl_gpu import dist as D
+        sizes = D.map_group_sizes(n, 5)
+        starts = np.cumsum([0] + sizes)
+        obs = [(int(starts[m]), sizes[m], O.OracleBatch(sizes[m], grid(f"map{m + 1}.txt"), 5, 20, 30,
+                                                         seed_base=42 + int(starts[m]), clear_on_reset=False))
+               for m in range(5)]
+    else:
+        obs = [(0, n, O.OracleBatch(n, grid("map1.txt"), 5, 20, 30, seed_base=42, clear_on_reset=False))]
     rs = np.random.RandomState(3)
     for k in range(45):
         acts = rs.randint(0, 15, size=(n, 5)).astype(np.uint8)
-        rr, sh, dn = ob.step(acts, auto_reset=True, consts=O.MAPPO_CONSTS)
+        parts = [ob.step(acts[b:b + m], auto_reset=True, consts=O.MAPPO_CONSTS) for b, m, ob in obs]
+        rr, sh, dn = (np.concatenate([p[i] for p in parts]) for i in range(3))
         np.testing.assert_array_equal(full[k, :, 0], rr)
         np.testing.assert_array_equal(full[k, :, 1], sh.astype(np.float64))
         np.testing.assert_array_equal(full[k, :, 2], dn.astype(np.float64))
@@ -105,3 +128,16 @@ def test_shard_partitions():
             assert ids == list(range(total))
     i, s = D.shard(4096, 3, 42)
     assert i[0] == 3 * 4096 and s[0] == 42 + 3 * 4096 and len(i) == 4096
+    # config 4: 13108 map1 envs then 13107 of each of map2..map5, contiguous;
+    # the ranks' blocks tile the global ids and each env keeps its global map and seed
+    assert D.map_group_sizes(65536, 5) == [13108, 13107, 13107, 13107, 13107]
+    for w in (1, 2, 3, 8):
+        all_ids, all_maps = [], []
+        for r in range(w):
+            ids, seeds, em, runs = D.shard_mixed(65536, 5, r, w, 42)
+            assert seeds == [42 + g for g in ids] and len(em) == len(ids)
+            assert sum(n for _, _, n in runs) == len(ids)
+            all_ids += ids
+            all_maps += em
+        assert all_ids == list(range(65536))
+        assert all_maps == sum([[m] * n for m, n in enumerate(D.map_group_sizes(65536, 5))], [])

@@ -39,3 +39,20 @@ def test_bench_two_ranks_strong_scaling():
     d = _run(["--total-envs", "1000"], 29563)
     assert d["scaling"] == "strong" and d["config"]["total_envs"] == 1000
     assert d["config"]["envs_per_gpu"] == 500
+
+
+def test_bench_two_ranks_config4_mixed_maps():
+    """BASELINE config 4's command at rehearsal size: map1..map5 groups over the ranks."""
+    d = _run(["--config", "4", "--total-envs", "2000"], 29565)
+    assert d["scaling"] == "strong" and d["config"]["total_envs"] == 2000 and d["config"]["envs_per_gpu"] == 1000
+    assert d["config"]["maps"] == [f"map{i}.txt" for i in range(1, 6)]
+    assert d["config"]["map_runs_rank0"] == [["map1.txt", 0, 400], ["map2.txt", 400, 400], ["map3.txt", 800, 200]]
+    assert d["value"] > 0
+
+
+def test_bench_two_ranks_config5():
+    """BASELINE config 5's command at rehearsal size: 64x64, 16 agents, 100 packages."""
+    d = _run(["--config", "5", "--total-envs", "1024"], 29567)
+    assert d["config"]["agents"] == 16 and d["config"]["packages"] == 100 and d["config"]["envs_per_gpu"] == 512
+    assert d["value"] > 0
+

@@ -6,12 +6,16 @@ import ctypes as C
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "mdl_engine.h")
+
+
+_REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _header_symbols():
@@ -129,3 +133,10 @@ def test_product_has_no_oracle_dependency():
         assert "mdl_oracle" not in txt and "liboracle" not in txt, f
     mk = open(os.path.join(REPO, "marl-delivery_amd", "Makefile")).read()
     assert "oracle" not in mk
+
+
+def test_bench_refuses_gpus_without_ranks():
+    """--gpus N needs N ranks: without torchrun the bench refuses instead of timing one GPU."""
+    out = subprocess.run([sys.executable, os.path.join(_REPO, "bench.py"), "--gpus", "2", "--steps", "5"], cwd=_REPO,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr

@@ -49,10 +49,29 @@ def test_encode_actions_codes_and_length_check():
         compat.encode_actions([("S", "0")], 2)
 
 
-def test_layout_aligns_parts():
-    offs, total = H._layout([(3, 1), (4, 2), (5, 4), (1, 1)])
-    assert offs == [0, 4, 8, 13] and total == 14
-    assert H._layout([]) == ([], 0)
+def test_align_and_c_packer_matches_numpy_layout():
+    """The helper functions' dict packer (CPython extension _mdl_pack) writes the view record
+    mdl_views_features reads: [t, A, n, map] + robots 0-indexed + tracker rows in dict order."""
+    assert [H._align(x) for x in (0, 1, 16, 17)] == [0, 16, 16, 32]
+    rs = np.random.RandomState(2)
+    for trial in range(20):
+        A, n, Hh, Ww = rs.randint(1, 9), rs.randint(0, 30), rs.randint(2, 30), rs.randint(2, 30)
+        robots = [(int(rs.randint(1, Hh + 1)), int(rs.randint(1, Ww + 1)), int(rs.randint(0, 5))) for _ in range(A)]
+        trk = {}
+        for j in rs.permutation(100)[:n]:
+            trk[int(j) + 1] = dict(id=int(j) + 1, status=("in_transit", "waiting")[rs.randint(2)],
+                                   start_pos=(int(rs.randint(Hh)), int(rs.randint(Ww))),
+                                   target_pos=(int(rs.randint(Hh)), int(rs.randint(Ww))),
+                                   start_time=int(rs.randint(50)), deadline=int(rs.randint(50, 500)))
+        rows = H._tracker_rows(trk)
+        want = np.concatenate([[7, A, n, 0], (np.array(robots) - [1, 1, 0]).reshape(-1),
+                               rows.reshape(-1)]).astype(np.int32)
+        assert np.array_equal(H.pack_view(7, robots, trk, Hh, Ww), want)        # dict, insertion order
+        assert np.array_equal(H.pack_view(7, robots, rows, Hh, Ww), want)       # rows
+    with pytest.raises(ValueError):
+        H.pack_view(0, [(0, 1, 0)], {}, 5, 5)                                    # 1-indexed cells
+    with pytest.raises(KeyError):
+        H.pack_view(0, [(1, 1, 0)], {1: dict(id=1, status="waiting")}, 5, 5)     # incomplete entry
 
 
 def test_pack_view_layout_and_checks():

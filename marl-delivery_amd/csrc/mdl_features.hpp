@@ -426,6 +426,58 @@ __device__ inline void emit_planes(const uint32_t* pl, int NW, int np, int HW, f
     }
 }
 
+// All 6A actor planes and the 4 critic planes straight from the five cell bitsets (maps too
+// large for prebuilt plane words, e.g. 64x64 with 16 agents): plane by plane (uniform loop),
+// float4 q of a plane is the 4 bits at bit 4q of its bit row -- word q/8 at shift 4(q%8), so with
+// q = lane + 64k the word is lane/8 + 8k and the shift is fixed per lane (no division per
+// float4).  The 4 bits are spread to bytes by one multiply and converted by v_cvt_f32_ubyteN.
+// Needs HW % 4 == 0 and 16-B aligned outputs (am / cm may be null).
+template <int B>
+__device__ __forceinline__ float cvt_ub(uint32_t y) {
+    float f;
+    if constexpr (B == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(y));
+    else if constexpr (B == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(f) : "v"(y));
+    else if constexpr (B == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(f) : "v"(y));
+    else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(f) : "v"(y));
+    return f;
+}
+
+__device__ inline void emit_maps_bitrows(const FeatLds& L, int NW, int HW, int A, float* am, float* cm) {
+    const int lane = lane_id();
+    const int qpp = HW >> 2;
+    const uint32_t sh = (uint32_t)(lane & 7) << 2;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const int np = 6 * A + 4;
+    for (int pl = 0; pl < np; pl++) {   // uniform
+        const bool actor = pl < 6 * A;
+        const int a = actor ? pl / 6 : 0, ch = actor ? pl - 6 * a : pl - 6 * A;
+        float* dst = actor ? (am ? am + (size_t)pl * HW : nullptr) : (cm ? cm + (size_t)ch * HW : nullptr);
+        if (!dst) continue;
+        // kind: 0 a bit row as is, 1 own-cell one-hot, 2 other robots, 5 carried-target one-hot
+        const int kind = actor ? (ch == 1 ? 1 : ch == 2 ? 2 : ch == 5 ? 5 : 0) : 0;
+        const int set = actor ? (ch == 0 ? BS_GRID : ch == 2 ? BS_ROBOT : ch == 3 ? BS_WSTART : BS_ATARGET)
+                              : (ch == 0 ? BS_GRID : ch == 1 ? BS_ROBOT : ch == 2 ? BS_WSTART : BS_ATARGET);
+        const int own = L.rcell[a], tgt = L.rtgt[a];
+        const uint32_t* row = L.bits + set * NW + (lane >> 3);
+        const uint32_t* mrow = L.bits + BS_MULTI * NW + (lane >> 3);
+        GLOBAL char* base = (GLOBAL char*)dst;
+        for (int q = lane, k = 0; q < qpp; q += WAVE, k += 8) {
+            const int c0 = q << 2;
+            uint32_t b;
+            if (kind == 1) {
+                b = onehot4(own, c0);
+            } else if (kind == 5) {
+                b = onehot4(tgt, c0);
+            } else {
+                b = __builtin_amdgcn_ubfe(row[k], sh, 4u);
+                if (kind == 2) b = (b & ~onehot4(own, c0)) | __builtin_amdgcn_ubfe(mrow[k], sh, 4u);
+            }
+            const uint32_t y = (b * 0x204081u) & 0x01010101u;   // bit i -> byte i (b < 16: no carries)
+            *(GLOBAL f32x4*)(base + ((uint32_t)q << 4)) = f32x4{cvt_ub<0>(y), cvt_ub<1>(y), cvt_ub<2>(y), cvt_ub<3>(y)};
+        }
+    }
+}
+
 // convert_observation for agents [a0, a0+na): dst [na][6][H][W].
 // a_valid=false reproduces the early return (channel 0 only).
 __device__ inline void emit_actor_maps(const FeatCtx& c, const FeatLds& L, int a0, int na, bool a_valid, float* dst) {

@@ -33,6 +33,11 @@
 #ifndef MDL_MOVE_PERM
 #define MDL_MOVE_PERM 1
 #endif
+// the general builder's maps straight from the cell bitsets (emit_maps_bitrows) when the
+// prebuilt plane words do not fit (64x64 maps)
+#ifndef MDL_OBS_BITROWS
+#define MDL_OBS_BITROWS 1
+#endif
 // Nearest waiting package of every agent from LDS-packed candidates (1) or one wave
 // reduction per agent (0) -- for the exact-A kernel of many robots (AU = 16, config 5:
 // 24.1 -> 22.1 us per step); with A <= 8 the LDS round trips on the latency-bound
@@ -1123,6 +1128,8 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
             feat_build_planes(c, L, planes);
             if (am) emit_planes(planes, c.NW, 6 * A, c.HW, am);
             if (cm) emit_planes(planes + 6 * A * c.NW, c.NW, 4, c.HW, cm);
+        } else if (MDL_OBS_BITROWS && (c.HW & 3) == 0 && (((uintptr_t)am | (uintptr_t)cm) & 15) == 0 && (am || cm)) {
+            emit_maps_bitrows(L, c.NW, c.HW, A, am, cm);
         } else {
             if (am) emit_actor_maps(c, L, 0, A, true, am);
             if (cm) emit_critic_map(c, L, cm);
@@ -1174,6 +1181,28 @@ __device__ inline ViewLdsPre view_carve(unsigned char* base, int NSmax) {
     return V;
 }
 
+// The rows of a view record whose header (A, ns) the caller has read (so the caller can put its
+// own independent loads beside these).
+__device__ inline TrkView load_view_rows(const int32_t* rec, int A, int ns, ViewLdsPre& V, int& cell, int& carry) {
+    const int lane = lane_id();
+    const int32_t* rb = rec + 4;
+    cell = 0;
+    carry = 0;
+    if (lane < A) {
+        cell = rb[3 * lane] | (rb[3 * lane + 1] << 8);
+        carry = rb[3 * lane + 2];
+    }
+    const int32_t* sl = rb + 3 * A;
+    for (int j = lane; j < ns; j += WAVE) {
+        const int32_t* s = sl + 8 * j;
+        V.ids[j] = s[0];
+        V.flag[j] = (uint8_t)(1 | (s[1] == ST_IN_TRANSIT ? 2 : 0));
+        V.pk[j] = pk_make(s[2] | (s[3] << 8), s[4] | (s[5] << 8), s[6], s[7]);
+    }
+    wave_sync();
+    return TrkView{V.ids, V.flag, V.pk, ns};
+}
+
 __device__ inline TrkView load_view(const int32_t* rec, ViewLdsPre& V, int& t, int& A, int& map, int& cell,
                                     int& carry) {
     const int lane = lane_id();
@@ -1212,8 +1241,12 @@ __global__ __launch_bounds__(256) void k_views_features(DevParams p, const int32
     if (wave >= wpb || w >= n) return;
     unsigned char* base = smem + (size_t)wave * lds_stride;
     ViewLdsPre V = view_carve(base, NSmax);
+    // every per-view input address / scalar first, in one round trip (the helpers pass host-mapped
+    // memory, where each dependent load is a PCIe round trip)
+    const int64_t off = offs[w];
+    const int a = agent_idx ? agent_idx[w] : 0;
     int t, A, map, cell, carry;
-    const TrkView trk = load_view(views + offs[w], V, t, A, map, cell, carry);
+    const TrkView trk = load_view(views + off, V, t, A, map, cell, carry);
     const MapDesc md = p.maps[map];
     FeatCtx c;
     c.A = A; c.NS = trk.n; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.NW = (c.HW + 31) / 32; c.t = t; c.T = T;
@@ -1224,7 +1257,6 @@ __global__ __launch_bounds__(256) void k_views_features(DevParams p, const int32
     FeatDims fd{64, NSmax, HW, MPc, MPsc, stage_floats(64, 1, MO, MPc, MR, MPsc)};
     FeatLds L = feat_carve(base + view_pre_bytes(NSmax), fd);
     feat_prepare(trk, c, L, cell, carry);
-    const int a = agent_idx ? agent_idx[w] : 0;
     const bool valid = a >= 0 && a < A;
     const int aa = valid ? a : 0;
     if (obs) emit_actor_maps(c, L, aa, 1, valid, obs + (size_t)w * 6 * c.HW);
@@ -1250,19 +1282,24 @@ __global__ __launch_bounds__(256) void k_views_shaped(DevParams p, const int32_t
     const int w = blockIdx.x * wpb + wave;
     if (wave >= wpb || w >= n) return;
     ViewLdsPre V = view_carve(smem + (size_t)wave * lds_stride, NSmax);
-    int t_prev, A, map, pcell, pcarry;
-    const TrkView trk = load_view(prev + prev_offs[w], V, t_prev, A, map, pcell, pcarry);
-    const int32_t* cr = cur + cur_offs[w];
-    const int t_cur = cr[0];
+    // every per-transition address / scalar first, in one round trip (host-mapped inputs: each
+    // dependent load is a PCIe round trip), then the current robots and actions beside the view
+    const int64_t po = prev_offs[w], co = cur_offs[w], ao = act_offs[w];
+    const double gw = g[w];
+    const int32_t* rec = prev + po;
+    const int32_t* cr = cur + co;
+    const int t_prev = rec[0], A = rec[1], ns = rec[2], t_cur = cr[0];   // the headers: one round trip
     const bool act = lane < A;
     int ccell = 0, ccarry = 0, mv = MV_S, op = 0;
-    if (act) {
+    if (act) {   // the current robots and actions, issued beside the view's rows
         ccell = cr[2 + 3 * lane] | (cr[3 + 3 * lane] << 8);
         ccarry = cr[4 + 3 * lane];
-        decode_action(acts[act_offs[w] + lane], 1, mv, op);
+        decode_action(acts[ao + lane], 1, mv, op);
     }
+    int pcell, pcarry;
+    const TrkView trk = load_view_rows(rec, A, ns, V, pcell, pcarry);
     const float s_a = shaped_agent(trk, C.c, act, pcell, pcarry, ccell, ccarry, mv, op, t_prev, t_cur);
-    const float res = (float)g[w] + np_sum_lanes(s_a, A);
+    const float res = (float)gw + np_sum_lanes(s_a, A);
     if (lane == 0) out[w] = res;
 }
 

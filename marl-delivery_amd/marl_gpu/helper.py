@@ -31,6 +31,7 @@ from .engine import MAPPO_SHAPING, QMIX_SHAPING, BatchedEnv
 from .compat import MOVE_CODES, OP_CODES
 
 _engines: dict = {}
+_CONSTS: dict = {}   # shaping-constant tuples -> their C double[9]
 
 
 def _engine_for(grid) -> BatchedEnv:
@@ -185,7 +186,12 @@ def shaped_rewards_views(g, prev_t, prev_robots1, cur_t, cur_robots1, action_cod
     u8[o_a:o_a + len(codes)] = np.frombuffer(codes, np.uint8)
     u8[o_off:o_off + 16] = 0
     u8[o_g:o_g + 8].view(np.float64)[0] = float(g)
-    cs = None if consts is None else (C.c_double * 9)(*[float(v) for v in consts])
+    cs = None
+    if consts is not None:
+        key = tuple(consts)
+        cs = _CONSTS.get(key)
+        if cs is None:
+            cs = _CONSTS[key] = (C.c_double * 9)(*[float(v) for v in consts])
     rc = ar._shaped(eng._h, b, b + o_off, ns, b + o_c, b + o_off, b + o_a, b + o_off, b + o_g, 1, cs, b + o_out,
                     _raw_stream(ar._dev))
     if rc:

@@ -6,7 +6,7 @@
   --config 3b  as 3 with the 1007-dim actor vector (MO=MP=100)
   --config 4   map1..map5 mixed, A=5, E=65536/8 per GPU (one GPU's shard), step only
   --config 5   synthetic 64x64, A=16, P=100, E=131072/8 per GPU, step; full observations per
-               chunk of 1024 envs
+               chunk of 4096 envs (MDL_OBS_CHUNK)
   --config rollout / rollout_graph   MAPPO rollout on the device
   --config alt      IDQ/qmix featurizers (§8(f)2)
   --config greedy   batched greedy baseline (§8(f)3)
@@ -140,7 +140,7 @@ def run(cfg, steps, warmup):
         # MO = 15 / MP = 20, critic map + MR = 16 / MPs = 100 vector) are 1.65 MB per env-step, so they
         # are built and reported per chunk of envs (general k_obs builder: A > 8, P > 64)
         H = W = 64
-        chunk = 1024
+        chunk = int(os.environ.get("MDL_OBS_CHUNK", "4096"))
         cb = env.obs_buffers(chunk, H, W)
         per_env = 4 * (A * 6 * H * W + A * env.actor_vec_dim + 4 * H * W + env.critic_vec_dim)
         for k in range(2):

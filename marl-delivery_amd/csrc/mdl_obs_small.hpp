@@ -163,6 +163,45 @@ __device__ __forceinline__ uint32_t bitonic_step(uint32_t x) {
     return sel64(bitonic_max_lanes<K, J>(), mn, mx);
 }
 
+// N independent wave sorts with their bitonic steps interleaved (each step applied to all N
+// keys before the next): the N chains' DPP / swizzle / bpermute latencies overlap.
+template <int N, int K, int J>
+__device__ __forceinline__ void bitonic_stepn(uint32_t (&x)[N]) {
+    uint32_t y[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) y[i] = xor_lane<J>(x[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t mn = x[i] < y[i] ? x[i] : y[i], mx = x[i] < y[i] ? y[i] : x[i];
+        x[i] = sel64(bitonic_max_lanes<K, J>(), mn, mx);
+    }
+}
+
+template <int N>
+__device__ inline void sort64_u32xn(uint32_t (&x)[N]) {
+    bitonic_stepn<N, 2, 1>(x);
+    bitonic_stepn<N, 4, 2>(x);
+    bitonic_stepn<N, 4, 1>(x);
+    bitonic_stepn<N, 8, 4>(x);
+    bitonic_stepn<N, 8, 2>(x);
+    bitonic_stepn<N, 8, 1>(x);
+    bitonic_stepn<N, 16, 8>(x);
+    bitonic_stepn<N, 16, 4>(x);
+    bitonic_stepn<N, 16, 2>(x);
+    bitonic_stepn<N, 16, 1>(x);
+    bitonic_stepn<N, 32, 16>(x);
+    bitonic_stepn<N, 32, 8>(x);
+    bitonic_stepn<N, 32, 4>(x);
+    bitonic_stepn<N, 32, 2>(x);
+    bitonic_stepn<N, 32, 1>(x);
+    bitonic_stepn<N, 64, 32>(x);
+    bitonic_stepn<N, 64, 16>(x);
+    bitonic_stepn<N, 64, 8>(x);
+    bitonic_stepn<N, 64, 4>(x);
+    bitonic_stepn<N, 64, 2>(x);
+    bitonic_stepn<N, 64, 1>(x);
+}
+
 // Ascending sort of one u32 per lane across the wave (bitonic network, 21 steps).
 __device__ inline uint32_t sort64_u32(uint32_t x) {
     x = bitonic_step<2, 1>(x);
@@ -197,8 +236,14 @@ __host__ __device__ inline size_t obs_small_lds_base(int A, int HW) {
     const int NW = (HW + 31) / 32;
     return (4 * (size_t)((6 * A + 9) * NW + 1) + 2 * 256 + 128 + 512 + 64 + 15) & ~(size_t)15;
 }
-// Floats per agent of the single-write image: self + MOc other-robot tuples, then MPc package slots.
-__host__ __device__ inline int obs_sw_stride(int MOc, int MPc) { return 6 + 5 * MOc + 5 * MPc; }
+// The single-write image: the float4-aligned covers ("windows") of the actor-vector slab's data
+// intervals -- per agent X(a) = its self / other-robot tuples with the previous agent's t/T, and
+// Pk(a) = its filled package slots, then the last t/T -- plus the interval -> window tables.
+// Upper bound of its float4s (each cover is at most len/4 + 2 float4s).
+__host__ __device__ inline int obs_sw_f4(int A, int MOc, int MPc) {
+    return A * ((7 + 5 * MOc) / 4 + 2 + (5 * MPc) / 4 + 2) + 2;
+}
+constexpr int OBS_SW_TAB = 16 * 2 * 8 + 16 * 3 * 8;   // bytes: [17] (q0, base) per interval, [17] windows
 // Whether the single-write path applies to this configuration (the device also needs a 16-B
 // aligned output, else it takes the early-fill path, which fits the same LDS slice).
 __host__ __device__ inline bool obs_sw_config(int A, int P, int MO, int MP) {
@@ -207,7 +252,7 @@ __host__ __device__ inline bool obs_sw_config(int A, int P, int MO, int MP) {
 }
 __host__ __device__ inline size_t obs_small_lds(int A, int HW, int P, int MO, int MP) {
     const int MOc = MO < A - 1 ? MO : A - 1, MPc = MP < P ? MP : P;
-    const size_t img = obs_sw_config(A, P, MO, MP) ? 4 * (((size_t)A * obs_sw_stride(MOc, MPc) + 3) & ~(size_t)3) : 0;
+    const size_t img = obs_sw_config(A, P, MO, MP) ? 16 * (size_t)obs_sw_f4(A, MOc, MPc) + OBS_SW_TAB : 0;
     return obs_small_lds_base(A, HW) + img;
 }
 
@@ -379,7 +424,16 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
                 key[a] = wt ? ((uint32_t)dlc << dsh) | (rk << 7) | ord7 : 0xffffffffu;
             }
         }
-        if (want <= 6) {
+        if (A == 5 && want > 6) {
+            // the configs' five agents: their sorts as five interleaved bitonic networks
+            uint32_t k5[5];
+#pragma unroll
+            for (int a = 0; a < 5; a++) k5[a] = key[a];
+            sort64_u32xn<5>(k5);
+#pragma unroll
+            for (int a = 0; a < 5; a++)
+                if (lane < want) invp[a * 64 + lane] = o2j[k5[a] & 127u];
+        } else if (want <= 6) {
             // a few slots: repeated wave minima (keys are unique)
             for (int s = 0; s < want; s++) {
 #pragma unroll
@@ -409,13 +463,51 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
         const int nq_o = A * A, ns = nq_o + A * MPc + A <= WAVE ? MPc : want;
         const int nq_p = A * ns, ntup = nq_o + nq_p + A;
         const float inv_a = 1.0f / (float)A, inv_w = ns > 0 ? 1.0f / (float)ns : 0.0f;
-        // single-write: agent a's data slots in the LDS image at img + a * L (zeroed first)
-        const int L = obs_sw_stride(MOc, MPc);
-        float* img = (float*)(smem_wave + obs_small_lds_base(A, HW));
+        // Single-write: the slab [g0, g0 + A*Dv) (float indices from avec) holds 2A+1 data intervals
+        // in order -- X(a) = [a*Dv - 1 (a > 0), a*Dv + 6 + 5MOc): agent a-1's t/T, agent a's self and
+        // filled other-robot tuples; Pk(a) = [a*Dv + 6 + 5MO, +5*want): its filled package slots; the
+        // last agent's t/T -- everything else is padding.  Each interval's float4 cover becomes a
+        // window of the LDS image (covers that share a float4 are merged), laid out exactly as the
+        // output, so the tuples are written into it and the slab is then streamed once: windows as
+        // float4 copies, the gaps between them as zero float4s.
+        const int g0 = w * A * Dv, S = A * Dv;
+        const int xe = 6 + 5 * MOc, ps0 = 6 + 5 * MO;
+        float4* img4 = reinterpret_cast<float4*>(smem_wave + obs_small_lds_base(A, HW));
+        int2* ktab = reinterpret_cast<int2*>(img4 + obs_sw_f4(A, MOc, MPc));   // interval k -> (cover q0, image base)
+        int4* wtab = reinterpret_cast<int4*>(ktab + 16 * 2 + 2);                // window -> (q0, q1, base)
+        int nwin = 0;
         if (sw) {
-            const int nz = (A * L + 3) >> 2;
-            for (int q = lane; q < nz; q += WAVE) reinterpret_cast<float4*>(img)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            int nf4 = 0, cq0 = 0, cq1 = 0, cbase = 0;
+            for (int k = 0; k <= 2 * A; k++) {   // uniform
+                const int a = k >> 1;
+                const int s0 = k == 2 * A ? S - 1 : (k & 1) ? a * Dv + ps0 : a * Dv - (a > 0 ? 1 : 0);
+                const int s1 = k == 2 * A ? S : (k & 1) ? s0 + 5 * want : a * Dv + xe;
+                if (s1 <= s0) continue;
+                const int qs = (g0 + s0) >> 2, qe = (g0 + s1 + 3) >> 2;
+                if (nwin > 0 && qs < cq1) {   // shares a float4 with the open window: merge
+                    cq1 = qe > cq1 ? qe : cq1;
+                } else {
+                    if (nwin > 0 && lane == 0) wtab[nwin - 1] = int4{cq0, cq1, cbase, 0};
+                    nf4 += cq1 - cq0;
+                    cq0 = qs;
+                    cq1 = qe;
+                    cbase = nf4;
+                    nwin++;
+                }
+                if (lane == 0) ktab[k] = int2{cq0, cbase};
+            }
+            if (lane == 0) wtab[nwin - 1] = int4{cq0, cq1, cbase, 0};
+            nf4 += cq1 - cq0;
+            for (int q = lane; q < nf4; q += WAVE) img4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
+        wave_sync();
+        // float f of the slab (interval k) -> its image float
+        auto img_at = [&](int k, int f) -> float* {
+            const int2 kt = ktab[k];
+            return reinterpret_cast<float*>(img4) + 4 * kt.y + (g0 + f - 4 * kt.x);
+        };
+        if (sw && lane < A)   // t/T of every agent: the first float of X(a+1), or the last interval
+            *img_at(lane + 1 < A ? 2 * (lane + 1) : 2 * A, lane * Dv + Dv - 1) = qdiv_r(t, yT);
         wave_sync();
 #ifndef MDL_EXP_NOWAIT   // profiling builds only (wrong results): no wait between the fill and the tuples
         if (av_early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slab's zeros are in L2
@@ -470,10 +562,12 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
 #ifdef MDL_EXP_NOTUPLES   // profiling builds only (wrong results): the actor vectors' tuples are not stored
             if (false) {
 #else
-            if ((ovalid && opos < MO) || is_p || is_s) {
+            // (single-write: empty package slots are zeros in the image already, and their interval
+            // may have no window)
+            if ((ovalid && opos < MO) || (is_p && (phas || !sw)) || is_s) {
 #endif
-                const int off = is_s ? 0 : is_o ? 6 + 5 * opos : 6 + 5 * (sw ? MOc : MO) + 5 * qb;
-                float* o = sw ? img + qa * L + off : av + qa * Dv + off;
+                const int off = is_s ? 0 : is_o ? 6 + 5 * opos : 6 + 5 * MO + 5 * qb;
+                float* o = sw ? img_at(is_p ? 2 * qa + 1 : 2 * qa, qa * Dv + off) : av + qa * Dv + off;
                 o[0] = d1;
                 o[1] = d2;
                 o[2] = is_p ? d3 : fl;
@@ -486,59 +580,29 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
             }
         }
         if (sw) {
-            // Stream the env's slab [g0, g0 + A*Dv) (floats from avec, 16-B aligned) once: the
-            // float4 covers of the data intervals -- X(a) = [a*Dv - 1, a*Dv + 6 + 5MOc) (the
-            // previous agent's t/T, self, filled other-robot slots), Pk(a) = [a*Dv + 6 + 5MO,
-            // +5*want) (filled package slots), the last agent's t/T -- from the image, every
-            // float4 between them as zeros.  Covers of neighbouring intervals may share a float4:
-            // both passes write the same complete value.  Only the slab's first / last float4 can
-            // hold another env's floats: those are written per float.
+            // Stream the slab once: every window's float4s from the image (a float4 that also holds
+            // another env's floats -- only at the slab's ends -- per float), the gap up to the next
+            // window as zeros.  The first window starts at the slab's first float4 and the last ends
+            // at its last, so every gap float4 lies inside the slab.
             wave_sync();
-            const float tval = qdiv_r(t, yT);
-            const int g0 = w * A * Dv, S = A * Dv;
-            const int xe = 6 + 5 * MOc, ps0 = 6 + 5 * MO, pe = 5 * MPc;
             float4* a4 = reinterpret_cast<float4*>(avec);
-            auto value = [&](int a, int o) -> float {   // float o of agent a's vector (o in [-4, Dv + 4))
-                const bool neg = o < 0;
-                const int aa = neg ? a - 1 : a, oo = neg ? o + Dv : o;
-                const bool inx = aa >= 0 && oo < xe, inp = aa >= 0 && (unsigned)(oo - ps0) < (unsigned)pe;
-                const float v = (inx || inp) ? img[aa * L + (inx ? oo : oo - (ps0 - xe))] : 0.0f;
-                return oo == Dv - 1 ? tval : v;
-            };
-            int qprev = g0 >> 2;   // end (float4 index) of the previous cover
-            for (int k = 0; k <= 2 * A; k++) {   // X(0), Pk(0), X(1), ..., Pk(A-1), then the last t/T
-                const int a = k >> 1;
-                int s0, s1;
-                if (k == 2 * A) {
-                    s0 = S - 1;
-                    s1 = S;
-                } else if (k & 1) {
-                    s0 = a * Dv + ps0;
-                    s1 = s0 + 5 * want;
-                } else {
-                    s0 = a * Dv - (a > 0 ? 1 : 0);
-                    s1 = a * Dv + xe;
-                }
-                if (s1 <= s0) continue;
-                const int qs = (g0 + s0) >> 2, qe = (g0 + s1 + 3) >> 2;
-                for (int q = qprev + lane; q < qs; q += WAVE) a4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                const int ab = k == 2 * A ? A - 1 : a;   // the agent the offsets below are relative to
-                for (int q = qs + lane; q < qe; q += WAVE) {
-                    const int f0 = 4 * q - g0;            // slab-relative index of the float4's first float
-                    const int o0 = f0 - ab * Dv;
-                    const float v0 = value(ab, o0), v1 = value(ab, o0 + 1), v2 = value(ab, o0 + 2),
-                                v3 = value(ab, o0 + 3);
+            for (int wi = 0; wi < nwin; wi++) {   // uniform
+                const int4 wt = wtab[wi];
+                for (int q = wt.x + lane; q < wt.y; q += WAVE) {
+                    const float4 v = img4[wt.z + (q - wt.x)];
+                    const int f0 = 4 * q - g0;   // slab-relative index of the float4's first float
                     if (f0 >= 0 && f0 + 4 <= S) {
-                        a4[q] = make_float4(v0, v1, v2, v3);
+                        a4[q] = v;
                     } else {
                         float* d = avec + 4 * (size_t)q;
-                        if ((unsigned)f0 < (unsigned)S) d[0] = v0;
-                        if ((unsigned)(f0 + 1) < (unsigned)S) d[1] = v1;
-                        if ((unsigned)(f0 + 2) < (unsigned)S) d[2] = v2;
-                        if ((unsigned)(f0 + 3) < (unsigned)S) d[3] = v3;
+                        if ((unsigned)f0 < (unsigned)S) d[0] = v.x;
+                        if ((unsigned)(f0 + 1) < (unsigned)S) d[1] = v.y;
+                        if ((unsigned)(f0 + 2) < (unsigned)S) d[2] = v.z;
+                        if ((unsigned)(f0 + 3) < (unsigned)S) d[3] = v.w;
                     }
                 }
-                qprev = qe > qprev ? qe : qprev;
+                const int gend = wi + 1 < nwin ? wtab[wi + 1].x : wt.y;
+                for (int q = wt.y + lane; q < gend; q += WAVE) a4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
         }
         // padding: other-robot slots [MOc, MO) and package slots [ns, MP) of every agent

@@ -21,6 +21,7 @@ should use BatchedEnv.build_obs instead.
 from __future__ import annotations
 
 import ctypes as C
+import struct
 
 import numpy as np
 
@@ -28,19 +29,28 @@ from . import _mdl_pack
 from ._lib import check, lib
 from ._lib import raw_stream as _raw_stream
 from .engine import MAPPO_SHAPING, QMIX_SHAPING, BatchedEnv
-from .compat import MOVE_CODES, OP_CODES
+from .compat import MOVE_CODES, OP_CODES, _code  # noqa: F401  (MOVE_CODES / OP_CODES re-exported)
 
 _engines: dict = {}
 _CONSTS: dict = {}   # shaping-constant tuples -> their C double[9]
 
 
+_last_grid: list = [None, None]   # [grid object, engine] of the previous call
+
+
 def _engine_for(grid) -> BatchedEnv:
+    """The helper engine of a map.  The reference's state dicts carry the env's own grid object
+    (``state['map']`` aliases ``env.grid``, env.py:140), so the same object is recognised by
+    identity first; any other grid is keyed by its contents."""
+    if grid is _last_grid[0]:
+        return _last_grid[1]
     g = np.asarray(grid, dtype=np.uint8)
     key = (g.shape, g.tobytes())
     eng = _engines.get(key)
     if eng is None:
         eng = BatchedEnv(g, 1, 1, 1, 2, tracker="fresh")
         _engines[key] = eng
+    _last_grid[0], _last_grid[1] = grid, eng
     return eng
 
 
@@ -102,6 +112,32 @@ def _align(x, a=16):
     return (x + a - 1) // a * a
 
 
+_OUT_NAMES = ("obs", "vec", "gmap", "gvec")
+_layouts: dict = {}
+
+
+def _features_layout(H, W, A, ns, n, MO, MP, MR, MPs, want):
+    """Byte offsets in the arena of one features call: view record, int64 offsets, agent
+    indices, then each wanted output (cached per shape)."""
+    key = (H, W, A, ns, n, MO, MP, MR, MPs, want)
+    lay = _layouts.get(key)
+    if lay is None:
+        sizes = {"obs": 6 * H * W, "vec": 6 + 5 * MO + 5 * MP + 1, "gmap": 4 * H * W, "gvec": 6 * MR + 7 * MPs + 1}
+        shapes = {"obs": (n, 6, H, W), "vec": (n, sizes["vec"]), "gmap": (n, 4, H, W), "gvec": (n, sizes["gvec"])}
+        vw = 4 + 3 * A + 8 * ns
+        o_off = _align(4 * vw)                      # int64 offsets (all 0: one shared record)
+        o_idx = _align(o_off + 8 * n)
+        pos = _align(o_idx + 4 * n)
+        outs = {}
+        for k in _OUT_NAMES:
+            if k in want:
+                outs[k] = (pos, 4 * n * sizes[k], shapes[k])
+                pos = _align(pos + 4 * n * sizes[k])
+        lay = _layouts[key] = (vw, o_off, o_idx, pos, outs,
+                               tuple(outs[k][0] if k in outs else None for k in _OUT_NAMES))
+    return lay
+
+
 def features(state, tracker, agent_indices, T, MO, MP, MR, MPs, want=("obs", "vec", "gmap", "gvec")):
     """Batched helper entry: one view per agent index (same state / tracker: one record that
     every view's offset points at).  ``tracker``: the reference's tracker dict (insertion order)
@@ -114,31 +150,21 @@ def features(state, tracker, agent_indices, T, MO, MP, MR, MPs, want=("obs", "ve
     robots = state["robots"]
     ns = len(tracker)
     n = len(agent_indices)
-    vw = 4 + 3 * len(robots) + 8 * ns
-    sizes = {"obs": 6 * H * W, "vec": 6 + 5 * MO + 5 * MP + 1, "gmap": 4 * H * W, "gvec": 6 * MR + 7 * MPs + 1}
-    names = [k for k in ("obs", "vec", "gmap", "gvec") if k in want]
-    o_off = _align(4 * vw)                      # int64 offsets (all 0: one shared record)
-    o_idx = _align(o_off + 8 * n)
-    pos = _align(o_idx + 4 * n)
-    o_out = {}
-    for k in names:
-        o_out[k] = pos
-        pos = _align(pos + 4 * n * sizes[k])
-    ar = _arena(eng)
-    u8 = ar.get(pos)
+    vw, o_off, o_idx, nbytes, outs, o_ptr = _features_layout(H, W, len(robots), ns, n, MO, MP, MR, MPs, tuple(want))
+    ar = eng.__dict__.get("_arena") or _arena(eng)
+    u8 = ar.get(nbytes)
     base = ar.addr
     _mdl_pack.pack_view(base, vw, int(state["time_step"]), robots, tracker, H, W, 0)
     u8[o_off:o_off + 8 * n] = 0
     u8[o_idx:o_idx + 4 * n].view(np.int32)[:] = agent_indices
     rc = ar._views(eng._h, base, base + o_off, n, ns, base + o_idx, int(T), MO, MP, MR, MPs,
-                   base + o_out["obs"] if "obs" in o_out else None, base + o_out["vec"] if "vec" in o_out else None,
-                   base + o_out["gmap"] if "gmap" in o_out else None, base + o_out["gvec"] if "gvec" in o_out else None,
+                   None if o_ptr[0] is None else base + o_ptr[0], None if o_ptr[1] is None else base + o_ptr[1],
+                   None if o_ptr[2] is None else base + o_ptr[2], None if o_ptr[3] is None else base + o_ptr[3],
                    _raw_stream(ar._dev))
     if rc:
         check(rc, "mdl_views_features")
     ar.wait()
-    shapes = {"obs": (n, 6, H, W), "vec": (n, sizes["vec"]), "gmap": (n, 4, H, W), "gvec": (n, sizes["gvec"])}
-    return {k: u8[o_out[k]:o_out[k] + 4 * n * sizes[k]].view(np.float32).reshape(shapes[k]).copy() for k in names}
+    return {k: u8[o:o + nb].view(np.float32).reshape(shape).copy() for k, (o, nb, shape) in outs.items()}
 
 
 def convert_observation(env_state_dict, persistent_packages_for_env, current_robot_idx):
@@ -168,36 +194,36 @@ def shaped_rewards_views(g, prev_t, prev_robots1, cur_t, cur_robots1, action_cod
     if not isinstance(tracker, dict):
         tracker = np.asarray(tracker, np.int64).reshape(-1, 8).tolist()
     ns = len(tracker)
-    A = len(prev_robots1)
-    vw = 4 + 3 * A + 8 * ns
-    cw = 2 + 3 * len(cur_robots1)
     codes = bytes(action_codes)
-    # arena: prev view | cur record | action bytes | three int64 offsets (0) | g (f64) | out (f32)
-    o_c = _align(4 * vw)
-    o_a = _align(o_c + 4 * cw)
-    o_off = _align(o_a + len(codes))
-    o_g = o_off + 16
-    o_out = o_g + 8
-    ar = _arena(eng)
-    u8 = ar.get(o_out + 16)
+    key = (len(prev_robots1), ns, len(cur_robots1), len(codes))
+    lay = _layouts.get(key)
+    if lay is None:   # arena: prev view | cur record | action bytes | three int64 offsets (0) | g (f64) | out (f32)
+        vw = 4 + 3 * key[0] + 8 * ns
+        cw = 2 + 3 * key[2]
+        o_c = _align(4 * vw)
+        o_a = _align(o_c + 4 * cw)
+        o_off = _align(o_a + key[3])
+        lay = _layouts[key] = (vw, cw, o_c, o_a, o_off, o_off + 24, o_off + 48)
+    vw, cw, o_c, o_a, o_off, o_out, nbytes = lay
+    ar = eng.__dict__.get("_arena") or _arena(eng)
+    u8 = ar.get(nbytes)
     b = ar.addr
     _mdl_pack.pack_view(b, vw, int(prev_t), prev_robots1, tracker, H, W, 0)
     _mdl_pack.pack_robots(b + o_c, cw, int(cur_t), cur_robots1)
     u8[o_a:o_a + len(codes)] = np.frombuffer(codes, np.uint8)
-    u8[o_off:o_off + 16] = 0
-    u8[o_g:o_g + 8].view(np.float64)[0] = float(g)
+    struct.pack_into("<qqd", u8, o_off, 0, 0, float(g))   # the offsets (all 0) and g
     cs = None
     if consts is not None:
-        key = tuple(consts)
-        cs = _CONSTS.get(key)
+        ck = tuple(consts)
+        cs = _CONSTS.get(ck)
         if cs is None:
-            cs = _CONSTS[key] = (C.c_double * 9)(*[float(v) for v in consts])
-    rc = ar._shaped(eng._h, b, b + o_off, ns, b + o_c, b + o_off, b + o_a, b + o_off, b + o_g, 1, cs, b + o_out,
-                    _raw_stream(ar._dev))
+            cs = _CONSTS[ck] = (C.c_double * 9)(*[float(v) for v in consts])
+    rc = ar._shaped(eng._h, b, b + o_off, ns, b + o_c, b + o_off, b + o_a, b + o_off, b + o_off + 16, 1, cs,
+                    b + o_out, _raw_stream(ar._dev))
     if rc:
         check(rc, "mdl_views_shaped_reward")
     ar.wait()
-    return np.float32(u8[o_out:o_out + 4].view(np.float32)[0])
+    return np.float32(struct.unpack_from("<f", u8, o_out)[0])
 
 
 def compute_shaped_rewards(global_reward, prev_env_state_dict, current_env_state_dict, actions_taken_for_all_agents,
@@ -208,8 +234,7 @@ def compute_shaped_rewards(global_reward, prev_env_state_dict, current_env_state
     defaults to a map large enough for the coordinates used."""
     prev_r = list(prev_env_state_dict["robots"])[:num_agents]
     cur_r = list(current_env_state_dict["robots"])[:num_agents]
-    codes = bytes(MOVE_CODES.get(m, 5) | (OP_CODES.get(o, 3) << 3)
-                  for m, o in list(actions_taken_for_all_agents)[:num_agents])
+    codes = bytes([_code(m, o) for m, o in list(actions_taken_for_all_agents)[:num_agents]])
     trk = persistent_packages_at_prev_state
     if grid is None:
         grid = prev_env_state_dict.get("map")

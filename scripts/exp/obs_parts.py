@@ -19,8 +19,10 @@ for k in range(60):
     env.step(torch.randint(0, 15, (E, A), dtype=torch.uint8, device="cuda", generator=g))
 bufs = env.obs_buffers()
 res = {}
-for which in [("actor_map",), ("actor_vec",), ("critic_map",), ("critic_vec",),
-              ("actor_map", "actor_vec", "critic_map", "critic_vec")]:
+ALL = [("actor_map",), ("actor_vec",), ("critic_map",), ("critic_vec",), ("actor_map", "actor_vec", "critic_map", "critic_vec")]
+sel = os.environ.get("OBS_WHICH")   # one subset only (PMC passes): "all" or an output name
+todo = ALL if not sel else [ALL[-1]] if sel == "all" else [(sel,)]
+for which in todo:
     for _ in range(3):
         env.build_obs(out=bufs, which=which)
     torch.cuda.synchronize()

@@ -33,6 +33,12 @@
 #ifndef MDL_MOVE_PERM
 #define MDL_MOVE_PERM 1
 #endif
+// Sixteen-robot pick-ups (config 5) from an LDS bitmap of the pickers' cells: waiting packages
+// test their start cell against it, and only the packages that sit under a picker are walked
+// (usually none or one) instead of two ballots and ~20 scalar ops for every robot that tries
+#ifndef MDL_PICK_BITS
+#define MDL_PICK_BITS 1
+#endif
 // the general builder's maps straight from the cell bitsets (emit_maps_bitrows) when the
 // prebuilt plane words do not fit (64x64 maps)
 #ifndef MDL_OBS_BITROWS
@@ -654,17 +660,54 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                 took[c] = 0;
             }
             int cnew = carry;
-            for (; pickers; pickers &= pickers - 1) {
-                const int i = ffs64(pickers);
-                const int ci = rdl(cell, i);
-                int fnd = -1;
+            bool by_bits = false;
+            if constexpr (AU == 16 && MDL_PICK_BITS) {
+                const MapDesc& md = p.maps[mi];
+                if (md.H <= 64 && md.W <= 64) {   // cells (r, c) -> bit r * 64 + c of a 4096-bit map
+                    by_bits = true;
+                    uint32_t* pb = (uint32_t*)(smem + (size_t)wave * lds_stride);
+                    auto bit_of = [](int cl) { return ((cl & 63) << 6) | ((cl >> 8) & 63); };
+                    wave_sync();
+                    reinterpret_cast<uint2*>(pb)[lane] = uint2{0u, 0u};
+                    wave_sync();
+                    if ((pickers >> lane) & 1ull) {
+                        const int ix = bit_of(cell);
+                        atomicOr(&pb[ix >> 5], 1u << (ix & 31));
+                    }
+                    wave_sync();
+                    uint64_t left = pickers;
 #pragma unroll
-                for (int c = 0; c < NCH; c++) {
-                    const uint64_t b = ballot(sw[c] == ci);
-                    took[c] |= fnd < 0 ? (b & (0ull - b)) : 0ull;
-                    fnd = (fnd < 0 && b != 0ull) ? c * WAVE + ffs64(b) : fnd;
+                    for (int c = 0; c < NCH; c++) {
+                        const int ix = bit_of(sw[c]);   // sw < 0: any in-range bit, masked below
+                        const uint64_t mt = ballot(sw[c] >= 0 && ((pb[ix >> 5] >> (ix & 31)) & 1u));
+                        // waiting packages under a picker, in index order: the first one at a
+                        // picker's cell is its lowest-index package (robot cells are distinct)
+                        for (uint64_t m = mt; m && left; m &= m - 1) {
+                            const int j = ffs64(m);
+                            const uint64_t who = ballot(cell == rdl(sw[c], j)) & left;
+                            if (who) {
+                                const int i = ffs64(who);
+                                left &= ~(1ull << i);
+                                took[c] |= 1ull << j;
+                                cnew = lane == i ? c * WAVE + j + 1 : cnew;
+                            }
+                        }
+                    }
                 }
-                cnew = lane == i ? fnd + 1 : cnew;  // not found: stays 0
+            }
+            if (!by_bits) {
+                for (; pickers; pickers &= pickers - 1) {
+                    const int i = ffs64(pickers);
+                    const int ci = rdl(cell, i);
+                    int fnd = -1;
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        const uint64_t b = ballot(sw[c] == ci);
+                        took[c] |= fnd < 0 ? (b & (0ull - b)) : 0ull;
+                        fnd = (fnd < 0 && b != 0ull) ? c * WAVE + ffs64(b) : fnd;
+                    }
+                    cnew = lane == i ? fnd + 1 : cnew;  // not found: stays 0
+                }
             }
             carry = cnew;
 #pragma unroll

@@ -188,6 +188,33 @@ int mdl_mail_export(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream);
  * `bytes` of it (16-byte aligned; a larger request replaces the arena, so earlier addresses die). */
 int mdl_host_arena(MdlEngine* eng, int64_t bytes, void** out);
 int mdl_host_wait(MdlEngine* eng, void* stream);
+/* mdl_views_features / mdl_views_shaped_reward with their inputs and outputs in the arena, and
+ * synchronous: the launch's own waves publish the arena's completion word when the last of them
+ * has written its outputs (no mdl_host_wait launch behind it), and the call returns once it has
+ * seen it.  `stream` need not be the caller's compute stream: nothing on the device waits for or
+ * on these calls.  (The helper functions of marl_gpu.helper call these from C, _mdl_pack.) */
+int mdl_host_views_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
+                            int32_t max_slots, const int32_t* agent_idx, int32_t T, int32_t MO, int32_t MP,
+                            int32_t MR, int32_t MPs, float* obs, float* vec, float* gmap, float* gvec, void* stream);
+int mdl_host_views_shaped_reward(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets,
+                                 int32_t max_slots, const int32_t* cur, const int64_t* cur_offsets,
+                                 const uint8_t* actions, const int64_t* act_offsets, const double* g, int32_t n,
+                                 const double* consts, float* out, void* stream);
+/* One view / one transition with its inputs in the caller's host memory (any: they are copied
+ * into the kernel's arguments at launch, so the wave reads them without round trips to host
+ * memory) and its outputs in the arena; synchronous as above.  rec: one view record (layout of
+ * mdl_views_features) of `words` <= MDL_VIEW_INLINE_WORDS words.  For the shaped reward the
+ * previous view, the current record and the action codes together must fit that capacity
+ * (prev_words + cur_words + ceil(n_actions / 4)); n_actions >= the view's robots.  Larger
+ * inputs take the arena entries above.  The shaped reward comes back beside the completion word,
+ * so `out` may be any host memory.  The single-call paths of marl_gpu.helper. */
+#define MDL_VIEW_INLINE_WORDS 768
+int mdl_host_view_features(MdlEngine* eng, const int32_t* rec, int32_t words, int32_t agent_index, int32_t T,
+                           int32_t MO, int32_t MP, int32_t MR, int32_t MPs, float* obs, float* vec, float* gmap,
+                           float* gvec, void* stream);
+int mdl_host_view_shaped_reward(MdlEngine* eng, const int32_t* prev_view, int32_t prev_words, const int32_t* cur,
+                                int32_t cur_words, const uint8_t* actions, int32_t n_actions, double g,
+                                const double* consts, float* out, void* stream);
 
 /* ---- checkpoint of the engine state ----
  * A versioned host blob: a 56-byte header (magic "MDLSTATE", version, E, A, P, T, tracker mode,

@@ -140,6 +140,8 @@ struct MdlEngine {
     void* arena = nullptr;
     size_t arena_bytes = 0;
     int32_t arena_seq = 0;
+    unsigned* arena_ctr = nullptr;     // device: waves of every self-publishing helper launch (mod 2^32)
+    unsigned arena_waves = 0;          // host mirror of *arena_ctr once the last such launch ended
 
     // (device pointer, bytes) of every state buffer, in checkpoint order
     // (the greedy agents' records follow when with_greedy: they exist once mdl_greedy_init ran)
@@ -625,8 +627,8 @@ int mail_finish(MdlEngine* eng, int32_t n, int32_t use_ids, hipStream_t s, const
     const int32_t want = eng->mail_seq = (eng->mail_seq % 0x7ffffff0) + 1;
     mdl::MailRows rows{m.seq, m.robots, m.pkgs, m.t, m.total_reward, m.rterms};
     const unsigned base = eng->mail_waves;
-    eng->mail_waves += mdl::mail_export_waves(n);   // the device counter's value after this launch
     HIPCHK(mdl::launch_mail_export(eng->p, use_ids ? m.ids : nullptr, n, rows, eng->mail_ctr, base, want, s));
+    eng->mail_waves += mdl::mail_export_waves(n);   // the device counter's value after this launch
     return spin_wait(m.seq, want, s, who);
 }
 }  // namespace
@@ -665,6 +667,7 @@ int mdl_host_arena(MdlEngine* eng, int64_t bytes, void** out) {
             (void)hipHostFree(eng->arena);
             eng->arena = nullptr;
         }
+        if (!eng->arena_ctr && eng->alloc(&eng->arena_ctr, 1)) return -1;
         void* a = nullptr;
         HIPCHK(hipHostMalloc(&a, cap + 256, hipHostMallocCoherent | hipHostMallocMapped));
         memset(a, 0, 256);
@@ -868,39 +871,162 @@ int mdl_read_state(MdlEngine* eng, int32_t* robots, int32_t* pkgs, int32_t* t, d
     return 0;
 }
 
-int mdl_views_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
-                       int32_t max_slots, const int32_t* agent_idx, int32_t T, int32_t MO, int32_t MP, int32_t MR,
-                       int32_t MPs, float* obs, float* vec, float* gmap, float* gvec, void* stream) {
-    if (!eng || !views || !offsets) return fail("mdl_views_features: null argument");
-    if (n_views < 0 || max_slots < 0 || max_slots > 4096) return fail("mdl_views_features: bad sizes");
-    if (MO < 0 || MP < 0 || MR < 0 || MPs < 0) return fail("mdl_views_features: negative slot count");
+namespace {
+// Helper calls that finish themselves (mdl_host_views_*): the launch's own waves publish the
+// arena's completion word, the host spins on it -- one launch, no k_publish behind it.
+struct HostCall {
+    MdlEngine* eng;
+    bool on;
+    mdl::Publish pb;
+    unsigned waves = 0;
+    HostCall(MdlEngine* e, bool publish) : eng(e), on(publish) {}
+    // the Publish of a launch of `launch_waves` waves
+    // (a one-wave launch publishes without the counter)
+    const mdl::Publish& arm(unsigned launch_waves) {
+        if (on) {
+            waves = launch_waves > 1 ? launch_waves : 0;
+            pb = mdl::Publish{(int32_t*)eng->arena, launch_waves > 1 ? eng->arena_ctr : nullptr, eng->arena_waves,
+                              (eng->arena_seq % 0x7ffffff0) + 1};
+        }
+        return pb;
+    }
+    // after a successful launch: account for its waves, then wait for its word
+    int finish(hipStream_t s, const char* who) {
+        if (!on) return 0;
+        eng->arena_seq = pb.value;
+        eng->arena_waves += waves;
+        return spin_wait(pb.seq, pb.value, s, who);
+    }
+};
+
+int views_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views, int32_t max_slots,
+                   const int32_t* agent_idx, int32_t T, int32_t MO, int32_t MP, int32_t MR, int32_t MPs, float* obs,
+                   float* vec, float* gmap, float* gvec, void* stream, bool host, const char* who) {
+    if (!eng || !views || !offsets) return fail("%s: null argument", who);
+    if (host && !eng->arena) return fail("%s: call mdl_host_arena first", who);
+    if (n_views < 0 || max_slots < 0 || max_slots > 4096) return fail("%s: bad sizes", who);
+    if (MO < 0 || MP < 0 || MR < 0 || MPs < 0) return fail("%s: negative slot count", who);
     if (n_views == 0) return 0;
     const int MPc = std::min(MP, max_slots), MPsc = std::min(MPs, max_slots);
     const size_t lds = mdl::views_lds(max_slots, eng->maxHW, MO, MPc, MR, MPsc);
     const int wpb = waves_per_block(lds);
-    if (wpb < 1) return fail("mdl_views_features: needs %zu bytes of LDS per view", lds);
+    if (wpb < 1) return fail("%s: needs %zu bytes of LDS per view", who, lds);
     DeviceGuard dg(eng->device);
+    HostCall hc(eng, host);
+    const hipStream_t s = (hipStream_t)stream;
     HIPCHK(mdl::launch_views_features(eng->p, views, offsets, n_views, agent_idx, T, MO, MP, MR, MPs, MPc, MPsc,
-                                      max_slots, eng->maxHW, obs, vec, gmap, gvec, wpb, lds, (hipStream_t)stream));
-    return 0;
+                                      max_slots, eng->maxHW, obs, vec, gmap, gvec, wpb, lds, s, hc.arm(mdl::grid_waves(n_views, wpb))));
+    return hc.finish(s, who);
 }
 
-int mdl_views_shaped_reward(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets,
-                            int32_t max_slots, const int32_t* cur, const int64_t* cur_offsets, const uint8_t* actions,
-                            const int64_t* act_offsets, const double* g, int32_t n, const double* consts, float* out,
-                            void* stream) {
+int views_shaped(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets, int32_t max_slots,
+                 const int32_t* cur, const int64_t* cur_offsets, const uint8_t* actions, const int64_t* act_offsets,
+                 const double* g, int32_t n, const double* consts, float* out, void* stream, bool host,
+                 const char* who) {
     if (!eng || !prev_views || !prev_offsets || !cur || !cur_offsets || !actions || !act_offsets || !g || !out)
-        return fail("mdl_views_shaped_reward: null argument");
-    if (n < 0 || max_slots < 0 || max_slots > 4096) return fail("mdl_views_shaped_reward: bad sizes");
+        return fail("%s: null argument", who);
+    if (host && !eng->arena) return fail("%s: call mdl_host_arena first", who);
+    if (n < 0 || max_slots < 0 || max_slots > 4096) return fail("%s: bad sizes", who);
     if (n == 0) return 0;
     mdl::ShapingConsts C;
     for (int i = 0; i < 9; i++) C.c[i] = consts ? (float)consts[i] : eng->p.shaping[i];
     const size_t lds = mdl::views_shaped_lds(max_slots);
     const int wpb = waves_per_block(lds);
     DeviceGuard dg(eng->device);
+    HostCall hc(eng, host);
+    const hipStream_t s = (hipStream_t)stream;
     HIPCHK(mdl::launch_views_shaped(eng->p, prev_views, prev_offsets, cur, cur_offsets, actions, act_offsets, g, n, C,
-                                    out, wpb, lds, max_slots, (hipStream_t)stream));
+                                    out, wpb, lds, max_slots, s, hc.arm(mdl::grid_waves(n, wpb))));
+    return hc.finish(s, who);
+}
+}  // namespace
+
+static_assert(mdl::VIEW_INLINE_WORDS == MDL_VIEW_INLINE_WORDS, "inline view capacity of the header and kernels");
+
+int mdl_host_view_features(MdlEngine* eng, const int32_t* rec, int32_t words, int32_t agent_index, int32_t T,
+                           int32_t MO, int32_t MP, int32_t MR, int32_t MPs, float* obs, float* vec, float* gmap,
+                           float* gvec, void* stream) {
+    const char* who = "mdl_host_view_features";
+    if (!eng || !rec) return fail("%s: null argument", who);
+    if (!eng->arena) return fail("%s: call mdl_host_arena first", who);
+    if (words < 4 || words > MDL_VIEW_INLINE_WORDS)
+        return fail("%s: a record of %d words (inline records hold 4..%d)", who, words, MDL_VIEW_INLINE_WORDS);
+    const int A = rec[1], ns = rec[2], map = rec[3];
+    if (A < 0 || A > MDL_MAX_ROBOTS || ns < 0 || 4 + 3 * A + 8 * ns > words)
+        return fail("%s: a record of %d words cannot hold %d robots and %d slots", who, words, A, ns);
+    if (map < 0 || map >= eng->p.n_maps) return fail("%s: map index %d out of range", who, map);
+    if (MO < 0 || MP < 0 || MR < 0 || MPs < 0) return fail("%s: negative slot count", who);
+    const int MPc = std::min(MP, ns), MPsc = std::min(MPs, ns);
+    const size_t lds = mdl::views_lds(ns, eng->maxHW, MO, MPc, MR, MPsc);
+    if (waves_per_block(lds) < 1) return fail("%s: needs %zu bytes of LDS", who, lds);
+    DeviceGuard dg(eng->device);
+    HostCall hc(eng, true);
+    const hipStream_t s = (hipStream_t)stream;
+    HIPCHK(mdl::launch_view_features_inline(eng->p, rec, words, agent_index, T, MO, MP, MR, MPs, MPc, MPsc, ns,
+                                            eng->maxHW, obs, vec, gmap, gvec, lds, s, hc.arm(1)));
+    return hc.finish(s, who);
+}
+
+int mdl_host_view_shaped_reward(MdlEngine* eng, const int32_t* prev_view, int32_t prev_words, const int32_t* cur,
+                                int32_t cur_words, const uint8_t* actions, int32_t n_actions, double g,
+                                const double* consts, float* out, void* stream) {
+    const char* who = "mdl_host_view_shaped_reward";
+    if (!eng || !prev_view || !cur || (!actions && n_actions > 0) || !out) return fail("%s: null argument", who);
+    if (!eng->arena) return fail("%s: call mdl_host_arena first", who);
+    if (prev_words < 4 || cur_words < 2 || n_actions < 0) return fail("%s: bad sizes", who);
+    const int A = prev_view[1], ns = prev_view[2];
+    if (A < 0 || A > MDL_MAX_ROBOTS || ns < 0 || 4 + 3 * A + 8 * ns > prev_words)
+        return fail("%s: a record of %d words cannot hold %d robots and %d slots", who, prev_words, A, ns);
+    if (cur[1] < A || 2 + 3 * A > cur_words || n_actions < A)
+        return fail("%s: %d robots before the step, but %d after and %d actions", who, A, cur[1], n_actions);
+    const int co = prev_words, ao = co + cur_words, words = ao + (n_actions + 3) / 4;
+    if (words > MDL_VIEW_INLINE_WORDS)
+        return fail("%s: %d words of inputs (inline records hold %d)", who, words, MDL_VIEW_INLINE_WORDS);
+    int32_t buf[MDL_VIEW_INLINE_WORDS];
+    memcpy(buf, prev_view, 4 * (size_t)prev_words);
+    memcpy(buf + co, cur, 4 * (size_t)cur_words);
+    buf[words - 1] = 0;
+    memcpy(buf + ao, actions, (size_t)n_actions);
+    mdl::ShapingConsts C;
+    for (int i = 0; i < 9; i++) C.c[i] = consts ? (float)consts[i] : eng->p.shaping[i];
+    const size_t lds = mdl::views_shaped_lds(ns);
+    DeviceGuard dg(eng->device);
+    HostCall hc(eng, true);
+    const hipStream_t s = (hipStream_t)stream;
+    HIPCHK(mdl::launch_view_shaped_inline(buf, words, co, ao, g, C, ns, lds, s, hc.arm(1)));
+    if (hc.finish(s, who)) return -1;
+    memcpy(out, (const int32_t*)eng->arena + 1, 4);   // the result, published beside the completion word
     return 0;
+}
+
+int mdl_views_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
+                       int32_t max_slots, const int32_t* agent_idx, int32_t T, int32_t MO, int32_t MP, int32_t MR,
+                       int32_t MPs, float* obs, float* vec, float* gmap, float* gvec, void* stream) {
+    return views_features(eng, views, offsets, n_views, max_slots, agent_idx, T, MO, MP, MR, MPs, obs, vec, gmap,
+                          gvec, stream, false, "mdl_views_features");
+}
+
+int mdl_host_views_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
+                            int32_t max_slots, const int32_t* agent_idx, int32_t T, int32_t MO, int32_t MP,
+                            int32_t MR, int32_t MPs, float* obs, float* vec, float* gmap, float* gvec, void* stream) {
+    return views_features(eng, views, offsets, n_views, max_slots, agent_idx, T, MO, MP, MR, MPs, obs, vec, gmap,
+                          gvec, stream, true, "mdl_host_views_features");
+}
+
+int mdl_views_shaped_reward(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets,
+                            int32_t max_slots, const int32_t* cur, const int64_t* cur_offsets, const uint8_t* actions,
+                            const int64_t* act_offsets, const double* g, int32_t n, const double* consts, float* out,
+                            void* stream) {
+    return views_shaped(eng, prev_views, prev_offsets, max_slots, cur, cur_offsets, actions, act_offsets, g, n, consts,
+                        out, stream, false, "mdl_views_shaped_reward");
+}
+
+int mdl_host_views_shaped_reward(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_offsets,
+                                 int32_t max_slots, const int32_t* cur, const int64_t* cur_offsets,
+                                 const uint8_t* actions, const int64_t* act_offsets, const double* g, int32_t n,
+                                 const double* consts, float* out, void* stream) {
+    return views_shaped(eng, prev_views, prev_offsets, max_slots, cur, cur_offsets, actions, act_offsets, g, n, consts,
+                        out, stream, true, "mdl_host_views_shaped_reward");
 }
 
 // ---- IDQ / qmix featurizers and IDQ reward shaping ----

@@ -17,6 +17,8 @@
 // k_step keeps the whole env in registers: robot a on lane a, package j on
 // lane j%64 of chunk j/64 (NCH chunks, compile-time).  Cross-lane work is
 // readlane / ballot only; LDS is touched only when an env resets.
+#include <cstring>
+
 #include "mdl_kernels.hpp"
 #include "mdl_features.hpp"
 #include "mdl_obs_small.hpp"
@@ -1271,25 +1273,32 @@ __device__ inline TrkView load_view(const int32_t* rec, ViewLdsPre& V, int& t, i
     return TrkView{V.ids, V.flag, V.pk, ns};
 }
 
-__global__ __launch_bounds__(256) void k_views_features(DevParams p, const int32_t* __restrict__ views,
-                                                        const int64_t* __restrict__ offs, int n,
-                                                        const int32_t* __restrict__ agent_idx, int T, int MO, int MP,
-                                                        int MR, int MPs, int MPc, int MPsc, int NSmax,
-                                                        float* __restrict__ obs, float* __restrict__ vec,
-                                                        float* __restrict__ gmap, float* __restrict__ gvec, int wpb,
-                                                        int lds_stride, int HW) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = wave_id();
-    const int w = blockIdx.x * wpb + wave;
-    if (wave >= wpb || w >= n) return;
-    unsigned char* base = smem + (size_t)wave * lds_stride;
+// the completion tail of a Publish launch (every wave of the grid runs it); a one-wave launch
+// (ctr == nullptr) publishes straight after its release
+__device__ __forceinline__ void publish_tail(const Publish& pb) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);   // this wave's stores, before it is counted
+    if (!pb.ctr) {
+        if (lane_id() == 0) __hip_atomic_store(pb.seq, pb.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (lane_id() == 0) {
+        const unsigned waves = gridDim.x * (blockDim.x / WAVE);
+        if (atomicAdd(pb.ctr, 1u) - pb.base == waves - 1u) {   // the last wave of the grid
+            __atomic_thread_fence(__ATOMIC_ACQ_REL);
+            __hip_atomic_store(pb.seq, pb.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// view record `rec`, agent index `a`, outputs row w
+__device__ __forceinline__ void views_features_one(const DevParams& p, const int32_t* rec, int w, int a, int T,
+                                                   int MO, int MP, int MR, int MPs, int MPc, int MPsc, int NSmax,
+                                                   float* __restrict__ obs, float* __restrict__ vec,
+                                                   float* __restrict__ gmap, float* __restrict__ gvec,
+                                                   unsigned char* base, int HW) {
     ViewLdsPre V = view_carve(base, NSmax);
-    // every per-view input address / scalar first, in one round trip (the helpers pass host-mapped
-    // memory, where each dependent load is a PCIe round trip)
-    const int64_t off = offs[w];
-    const int a = agent_idx ? agent_idx[w] : 0;
     int t, A, map, cell, carry;
-    const TrkView trk = load_view(views + off, V, t, A, map, cell, carry);
+    const TrkView trk = load_view(rec, V, t, A, map, cell, carry);
     const MapDesc md = p.maps[map];
     FeatCtx c;
     c.A = A; c.NS = trk.n; c.H = md.H; c.W = md.W; c.HW = md.H * md.W; c.NW = (c.HW + 31) / 32; c.t = t; c.T = T;
@@ -1311,6 +1320,61 @@ __global__ __launch_bounds__(256) void k_views_features(DevParams p, const int32
     if (gvec) emit_critic_vec(trk, c, L, gvec + (size_t)w * (6 * MR + 7 * MPs + 1));
 }
 
+__global__ __launch_bounds__(256) void k_views_features(DevParams p, const int32_t* __restrict__ views,
+                                                        const int64_t* __restrict__ offs, int n,
+                                                        const int32_t* __restrict__ agent_idx, int T, int MO, int MP,
+                                                        int MR, int MPs, int MPc, int MPsc, int NSmax,
+                                                        float* __restrict__ obs, float* __restrict__ vec,
+                                                        float* __restrict__ gmap, float* __restrict__ gvec, int wpb,
+                                                        int lds_stride, int HW, Publish pb) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int wave = wave_id();
+    const int w = blockIdx.x * wpb + wave;
+    if (wave < wpb && w < n) {
+        // every per-view input address / scalar first, in one round trip (the helpers pass host-mapped
+        // memory, where each dependent load is a PCIe round trip)
+        const int64_t off = offs[w];
+        const int a = agent_idx ? agent_idx[w] : 0;
+        views_features_one(p, views + off, w, a, T, MO, MP, MR, MPs, MPc, MPsc, NSmax, obs, vec, gmap, gvec,
+                           smem + (size_t)wave * lds_stride, HW);
+    }
+    if (pb.seq) publish_tail(pb);
+}
+
+// One view whose record travels in the kernel arguments (mdl_host_view_features): the launch
+// copies it into the kernarg segment, so the wave reads it from there instead of making
+// dependent round trips to host memory.  One wave, one block.
+template <int CAP>
+__global__ __launch_bounds__(64) void k_view_features_inl(DevParams p, int a, int T, int MO, int MP, int MR, int MPs,
+                                                          int MPc, int MPsc, int NSmax, float* __restrict__ obs,
+                                                          float* __restrict__ vec, float* __restrict__ gmap,
+                                                          float* __restrict__ gvec, int HW, Publish pb,
+                                                          ViewInline<CAP> rec) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    views_features_one(p, rec.w, 0, a, T, MO, MP, MR, MPs, MPc, MPsc, NSmax, obs, vec, gmap, gvec, smem, HW);
+    if (pb.seq) publish_tail(pb);
+}
+
+// one transition: prev view record, current record [t, A] + A x 3, action codes, global reward
+__device__ __forceinline__ float views_shaped_one(const int32_t* rec, const int32_t* cr, const uint8_t* acts,
+                                                  double gw, const ShapingConsts& C, unsigned char* base,
+                                                  int NSmax) {
+    const int lane = lane_id();
+    ViewLdsPre V = view_carve(base, NSmax);
+    const int t_prev = rec[0], A = rec[1], ns = rec[2], t_cur = cr[0];   // the headers: one round trip
+    const bool act = lane < A;
+    int ccell = 0, ccarry = 0, mv = MV_S, op = 0;
+    if (act) {   // the current robots and actions, issued beside the view's rows
+        ccell = cr[2 + 3 * lane] | (cr[3 + 3 * lane] << 8);
+        ccarry = cr[4 + 3 * lane];
+        decode_action(acts[lane], 1, mv, op);
+    }
+    int pcell, pcarry;
+    const TrkView trk = load_view_rows(rec, A, ns, V, pcell, pcarry);
+    const float s_a = shaped_agent(trk, C.c, act, pcell, pcarry, ccell, ccarry, mv, op, t_prev, t_cur);
+    return (float)gw + np_sum_lanes(s_a, A);
+}
+
 __global__ __launch_bounds__(256) void k_views_shaped(DevParams p, const int32_t* __restrict__ prev,
                                                       const int64_t* __restrict__ prev_offs,
                                                       const int32_t* __restrict__ cur,
@@ -1318,32 +1382,36 @@ __global__ __launch_bounds__(256) void k_views_shaped(DevParams p, const int32_t
                                                       const uint8_t* __restrict__ acts,
                                                       const int64_t* __restrict__ act_offs,
                                                       const double* __restrict__ g, int n, ShapingConsts C,
-                                                      float* __restrict__ out, int wpb, int lds_stride, int NSmax) {
+                                                      float* __restrict__ out, int wpb, int lds_stride, int NSmax,
+                                                      Publish pb) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int wave = wave_id();
-    const int lane = lane_id();
     const int w = blockIdx.x * wpb + wave;
-    if (wave >= wpb || w >= n) return;
-    ViewLdsPre V = view_carve(smem + (size_t)wave * lds_stride, NSmax);
-    // every per-transition address / scalar first, in one round trip (host-mapped inputs: each
-    // dependent load is a PCIe round trip), then the current robots and actions beside the view
-    const int64_t po = prev_offs[w], co = cur_offs[w], ao = act_offs[w];
-    const double gw = g[w];
-    const int32_t* rec = prev + po;
-    const int32_t* cr = cur + co;
-    const int t_prev = rec[0], A = rec[1], ns = rec[2], t_cur = cr[0];   // the headers: one round trip
-    const bool act = lane < A;
-    int ccell = 0, ccarry = 0, mv = MV_S, op = 0;
-    if (act) {   // the current robots and actions, issued beside the view's rows
-        ccell = cr[2 + 3 * lane] | (cr[3 + 3 * lane] << 8);
-        ccarry = cr[4 + 3 * lane];
-        decode_action(acts[ao + lane], 1, mv, op);
+    if (wave < wpb && w < n) {
+        // every per-transition address / scalar first, in one round trip (host-mapped inputs: each
+        // dependent load is a PCIe round trip)
+        const int64_t po = prev_offs[w], co = cur_offs[w], ao = act_offs[w];
+        const double gw = g[w];
+        const float res = views_shaped_one(prev + po, cur + co, acts + ao, gw, C, smem + (size_t)wave * lds_stride,
+                                           NSmax);
+        if (lane_id() == 0) out[w] = res;
     }
-    int pcell, pcarry;
-    const TrkView trk = load_view_rows(rec, A, ns, V, pcell, pcarry);
-    const float s_a = shaped_agent(trk, C.c, act, pcell, pcarry, ccell, ccarry, mv, op, t_prev, t_cur);
-    const float res = (float)gw + np_sum_lanes(s_a, A);
-    if (lane == 0) out[w] = res;
+    if (pb.seq) publish_tail(pb);
+}
+
+// One transition whose inputs travel in the kernel arguments (mdl_host_view_shaped_reward):
+// rec = prev view | current record at word co | action codes at word ao.  One wave, one block.
+// The result travels with the completion word: one 64-bit store of (seq, result bits) to the
+// 8-byte-aligned pb.seq, so no store has to be ordered before it (no release fence).
+template <int CAP>
+__global__ __launch_bounds__(64) void k_view_shaped_inl(double g, ShapingConsts C, int co, int ao, int NSmax,
+                                                        Publish pb, ViewInline<CAP> rec) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const float res = views_shaped_one(rec.w, rec.w + co, (const uint8_t*)(rec.w + ao), g, C, smem, NSmax);
+    if (lane_id() == 0) {
+        const uint64_t v = (uint64_t)(uint32_t)pb.value | ((uint64_t)__float_as_uint(res) << 32);
+        __hip_atomic_store((uint64_t*)pb.seq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ------------------------------------------------- IDQ / qmix featurizers
@@ -1557,14 +1625,7 @@ __global__ __launch_bounds__(256) void k_mail_export(DevParams p, const int32_t*
             m.rterms[w] = (int32_t)s.ctr;
         }
     }
-    __atomic_thread_fence(__ATOMIC_RELEASE);   // this wave's mailbox stores, before it is counted
-    if (lane == 0) {
-        const unsigned waves = gridDim.x * 4u;
-        if (atomicAdd(ctr, 1u) - base == waves - 1u) {   // the last wave of the grid: every row is out
-            __atomic_thread_fence(__ATOMIC_ACQ_REL);
-            __hip_atomic_store(m.seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
+    publish_tail(Publish{m.seq, ctr, base, seq});   // the last wave: every row is out
 }
 
 // one wave: publish `seq` (host-mapped) once every kernel queued before it on the stream has
@@ -1582,6 +1643,7 @@ hipError_t launch_publish(int32_t* seq, int32_t value, hipStream_t s) {
 }
 
 unsigned mail_export_waves(int n) { return 4u * (unsigned)blocks_for(n > 0 ? n : 1, 4); }
+unsigned grid_waves(int n, int wpb) { return 4u * (unsigned)blocks_for(n, wpb); }
 
 hipError_t launch_mail_export(const DevParams& p, const int32_t* ids, int n, const MailRows& m, unsigned* ctr,
                               unsigned base, int32_t seq, hipStream_t s) {
@@ -1777,18 +1839,52 @@ hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, flo
 hipError_t launch_views_features(const DevParams& p, const int32_t* views, const int64_t* offs, int n,
                                  const int32_t* agent_idx, int T, int MO, int MP, int MR, int MPs, int MPc, int MPsc,
                                  int NSmax, int HW, float* obs, float* vec, float* gmap, float* gvec, int wpb,
-                                 size_t lds, hipStream_t s) {
+                                 size_t lds, hipStream_t s, const Publish& pb) {
     hipLaunchKernelGGL(k_views_features, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, views, offs, n,
-                       agent_idx, T, MO, MP, MR, MPs, MPc, MPsc, NSmax, obs, vec, gmap, gvec, wpb, (int)lds, HW);
+                       agent_idx, T, MO, MP, MR, MPs, MPc, MPsc, NSmax, obs, vec, gmap, gvec, wpb, (int)lds, HW, pb);
+    return hipGetLastError();
+}
+
+hipError_t launch_view_features_inline(const DevParams& p, const int32_t* rec, int words, int a, int T, int MO,
+                                      int MP, int MR, int MPs, int MPc, int MPsc, int NSmax, int HW, float* obs,
+                                      float* vec, float* gmap, float* gvec, size_t lds, hipStream_t s,
+                                      const Publish& pb) {
+    if (words <= VIEW_INLINE_SMALL) {
+        ViewInline<VIEW_INLINE_SMALL> r;
+        std::memcpy(r.w, rec, 4 * (size_t)words);
+        hipLaunchKernelGGL(k_view_features_inl<VIEW_INLINE_SMALL>, dim3(1), dim3(64), lds, s, p, a, T, MO, MP, MR,
+                           MPs, MPc, MPsc, NSmax, obs, vec, gmap, gvec, HW, pb, r);
+    } else {
+        ViewInline<VIEW_INLINE_WORDS> r;
+        std::memcpy(r.w, rec, 4 * (size_t)words);
+        hipLaunchKernelGGL(k_view_features_inl<VIEW_INLINE_WORDS>, dim3(1), dim3(64), lds, s, p, a, T, MO, MP, MR,
+                           MPs, MPc, MPsc, NSmax, obs, vec, gmap, gvec, HW, pb, r);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_view_shaped_inline(const int32_t* rec, int words, int co, int ao, double g, const ShapingConsts& C,
+                                     int NSmax, size_t lds, hipStream_t s, const Publish& pb) {
+    if (words <= VIEW_INLINE_SMALL) {
+        ViewInline<VIEW_INLINE_SMALL> r;
+        std::memcpy(r.w, rec, 4 * (size_t)words);
+        hipLaunchKernelGGL(k_view_shaped_inl<VIEW_INLINE_SMALL>, dim3(1), dim3(64), lds, s, g, C, co, ao, NSmax, pb,
+                           r);
+    } else {
+        ViewInline<VIEW_INLINE_WORDS> r;
+        std::memcpy(r.w, rec, 4 * (size_t)words);
+        hipLaunchKernelGGL(k_view_shaped_inl<VIEW_INLINE_WORDS>, dim3(1), dim3(64), lds, s, g, C, co, ao, NSmax, pb,
+                           r);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_views_shaped(const DevParams& p, const int32_t* prev, const int64_t* prev_offs, const int32_t* cur,
                                const int64_t* cur_offs, const uint8_t* acts, const int64_t* act_offs, const double* g,
                                int n, const ShapingConsts& C, float* out, int wpb, size_t lds, int NSmax,
-                               hipStream_t s) {
+                               hipStream_t s, const Publish& pb) {
     hipLaunchKernelGGL(k_views_shaped, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, prev, prev_offs, cur,
-                       cur_offs, acts, act_offs, g, n, C, out, wpb, (int)lds, NSmax);
+                       cur_offs, acts, act_offs, g, n, C, out, wpb, (int)lds, NSmax, pb);
     return hipGetLastError();
 }
 

@@ -24,14 +24,39 @@ hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, 
                            size_t lds, hipStream_t s);
 hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
                       int wpb, size_t lds, hipStream_t s);
+// A launch's own completion word (host-mapped): every wave of its grid counts itself in the
+// running device counter `ctr` (never reset: `base` is its value before the launch) after a
+// system-scope release of its stores; the last one writes `value` to `seq`.  seq == nullptr: none;
+// ctr == nullptr: a one-wave launch, which writes `value` straight after its release.
+struct Publish {
+    int32_t* seq = nullptr;
+    unsigned* ctr = nullptr;
+    unsigned base = 0;
+    int32_t value = 0;
+};
+// A view record carried in the kernel arguments (mdl_host_view_*): two capacity classes, the larger
+// sized so the kernel's whole argument block stays well inside the 4 KiB kernarg limit.
+constexpr int VIEW_INLINE_SMALL = 256, VIEW_INLINE_WORDS = 768;
+template <int CAP>
+struct ViewInline {
+    int32_t w[CAP];
+};
+hipError_t launch_view_features_inline(const DevParams& p, const int32_t* rec, int words, int a, int T, int MO,
+                                      int MP, int MR, int MPs, int MPc, int MPsc, int NSmax, int HW, float* obs,
+                                      float* vec, float* gmap, float* gvec, size_t lds, hipStream_t s,
+                                      const Publish& pb);
+// the result comes back in the completion word's second half (pb.seq 8-byte aligned)
+hipError_t launch_view_shaped_inline(const int32_t* rec, int words, int co, int ao, double g, const ShapingConsts& C,
+                                     int NSmax, size_t lds, hipStream_t s, const Publish& pb);
+unsigned grid_waves(int n, int wpb);   // waves of a 256-thread-block launch of wpb views per block
 hipError_t launch_views_features(const DevParams& p, const int32_t* views, const int64_t* offs, int n,
                                  const int32_t* agent_idx, int T, int MO, int MP, int MR, int MPs, int MPc, int MPsc,
                                  int NSmax, int HW, float* obs, float* vec, float* gmap, float* gvec, int wpb,
-                                 size_t lds, hipStream_t s);
+                                 size_t lds, hipStream_t s, const Publish& pb = Publish{});
 hipError_t launch_views_shaped(const DevParams& p, const int32_t* prev, const int64_t* prev_offs, const int32_t* cur,
                                const int64_t* cur_offs, const uint8_t* acts, const int64_t* act_offs, const double* g,
                                int n, const ShapingConsts& C, float* out, int wpb, size_t lds, int NSmax,
-                               hipStream_t s);
+                               hipStream_t s, const Publish& pb = Publish{});
 // the dict-API mailbox's output rows (host-mapped memory; row w = the w-th env of a call)
 struct MailRows {
     int32_t* seq;      // completion word, written last

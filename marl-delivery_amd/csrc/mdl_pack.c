@@ -9,6 +9,11 @@
  * reference's whole CPU helper; this walks the dicts once and writes the words straight into the
  * engine's host-mapped arena (an address the caller passes), so the kernel reads them from there.
  *
+ * features() / shaped() go one step further for the single-view helper calls: pack, launch through
+ * the engine's self-publishing entries (mdl_host_views_features / mdl_host_views_shaped_reward,
+ * whose addresses bind() receives once), wait, and return the numpy outputs -- no ctypes call and
+ * no Python-level buffer handling per call.
+ *
  * Host plumbing only (no GPU code, no reference semantics beyond the record layout).  The tracker
  * dict is read in insertion order (PyDict_Next), the order the reference iterates
  * persistent_packages.values() in (MAPPO/trainer.py:95-130); 'status' == 'in_transit' -> 2, else 1.
@@ -16,6 +21,12 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <stdint.h>
+#include <string.h>
+#define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
+#include <numpy/arrayobject.h>
+#include <numpy/arrayscalars.h>
+
+#include "mdl_engine.h"   /* MDL_VIEW_INLINE_WORDS */
 
 static int get_int(PyObject* o, long* out) {
     long v = PyLong_AsLong(o);
@@ -71,20 +82,17 @@ static int dict_pair(PyObject* d, PyObject* key, long* a, long* b) {
     return 0;
 }
 
-/* pack_view(addr, cap_words, t, robots, tracker, H, W, map_index) -> words written.
- * robots: sequence of (row, col, carrying) 1-indexed; tracker: dict id -> entry dict in insertion order
- * (MAPPO/trainer.py:95-130 layout), or a sequence of rows (id, status, sr, sc, tr, tc, st, dl). */
-static PyObject* pack_view(PyObject* self, PyObject* args) {
-    unsigned long long addr;
-    Py_ssize_t cap;
-    long t, H, W, map_index;
-    PyObject *robots, *tracker;
-    (void)self;
-    if (!PyArg_ParseTuple(args, "KnlOOlll", &addr, &cap, &t, &robots, &tracker, &H, &W, &map_index)) return NULL;
-    int32_t* w = (int32_t*)(uintptr_t)addr;
+/* The view record [t, A, n, map] + A x (row, col, carrying) 0-indexed + n x (id, status, sr, sc, tr, tc,
+ * st, dl) at w (cap words), from the first `amax` robots (amax < 0: all).  robots: sequence of
+ * (row, col, carrying) 1-indexed; tracker: dict id -> entry dict in insertion order
+ * (MAPPO/trainer.py:95-130 layout), or a sequence of rows.  Returns the words written, or -1 with an
+ * exception set. */
+static Py_ssize_t do_pack_view(int32_t* w, Py_ssize_t cap, long t, PyObject* robots, PyObject* tracker, long H,
+                               long W, long map_index, Py_ssize_t amax) {
     PyObject* rs = PySequence_Fast(robots, "robots must be a sequence");
-    if (!rs) return NULL;
-    const Py_ssize_t A = PySequence_Fast_GET_SIZE(rs);
+    if (!rs) return -1;
+    Py_ssize_t A = PySequence_Fast_GET_SIZE(rs);
+    if (amax >= 0 && amax < A) A = amax;
     const int is_dict = PyDict_Check(tracker);
     PyObject* ts = NULL;
     Py_ssize_t n;
@@ -94,11 +102,11 @@ static PyObject* pack_view(PyObject* self, PyObject* args) {
         ts = PySequence_Fast(tracker, "tracker must be a dict or a sequence of rows");
         if (!ts) {
             Py_DECREF(rs);
-            return NULL;
+            return -1;
         }
         n = PySequence_Fast_GET_SIZE(ts);
     }
-    PyObject* ret = NULL;
+    Py_ssize_t ret = -1;
     if (A > 64) {
         PyErr_SetString(PyExc_ValueError, "at most 64 robots per view");
         goto done;
@@ -166,31 +174,37 @@ static PyObject* pack_view(PyObject* self, PyObject* args) {
         o += 8;
         k++;
     }
-    ret = PyLong_FromSsize_t(4 + 3 * A + 8 * n);
+    ret = 4 + 3 * A + 8 * n;
 done:
     Py_DECREF(rs);
     Py_XDECREF(ts);
     return ret;
 }
 
-/* pack_robots(addr, cap_words, t, robots) -> words: [t, A] + A x (row, col, carrying) 0-indexed
- * (the "current state" record of mdl_views_shaped_reward). */
-static PyObject* pack_robots(PyObject* self, PyObject* args) {
+/* pack_view(addr, cap_words, t, robots, tracker, H, W, map_index) -> words written. */
+static PyObject* pack_view(PyObject* self, PyObject* args) {
     unsigned long long addr;
     Py_ssize_t cap;
-    long t;
-    PyObject* robots;
+    long t, H, W, map_index;
+    PyObject *robots, *tracker;
     (void)self;
-    if (!PyArg_ParseTuple(args, "KnlO", &addr, &cap, &t, &robots)) return NULL;
+    if (!PyArg_ParseTuple(args, "KnlOOlll", &addr, &cap, &t, &robots, &tracker, &H, &W, &map_index)) return NULL;
+    const Py_ssize_t nw = do_pack_view((int32_t*)(uintptr_t)addr, cap, t, robots, tracker, H, W, map_index, -1);
+    return nw < 0 ? NULL : PyLong_FromSsize_t(nw);
+}
+
+/* [t, A] + A x (row, col, carrying) 0-indexed at w from the first `amax` robots (amax < 0: all)
+ * (the "current state" record of mdl_views_shaped_reward).  Returns the words, or -1. */
+static Py_ssize_t do_pack_robots(int32_t* w, Py_ssize_t cap, long t, PyObject* robots, Py_ssize_t amax) {
     PyObject* rs = PySequence_Fast(robots, "robots must be a sequence");
-    if (!rs) return NULL;
-    const Py_ssize_t A = PySequence_Fast_GET_SIZE(rs);
+    if (!rs) return -1;
+    Py_ssize_t A = PySequence_Fast_GET_SIZE(rs);
+    if (amax >= 0 && amax < A) A = amax;
     if (2 + 3 * A > cap) {
         Py_DECREF(rs);
         PyErr_SetString(PyExc_ValueError, "record larger than the arena");
-        return NULL;
+        return -1;
     }
-    int32_t* w = (int32_t*)(uintptr_t)addr;
     w[0] = (int32_t)t;
     w[1] = (int32_t)A;
     for (Py_ssize_t i = 0; i < A; i++) {
@@ -198,24 +212,285 @@ static PyObject* pack_robots(PyObject* self, PyObject* args) {
         PyObject* rb = PySequence_Fast_GET_ITEM(rs, i);
         if (seq_int(rb, 0, &r) || seq_int(rb, 1, &c) || seq_int(rb, 2, &cy)) {
             Py_DECREF(rs);
-            return NULL;
+            return -1;
         }
         w[2 + 3 * i] = (int32_t)(r - 1);
         w[3 + 3 * i] = (int32_t)(c - 1);
         w[4 + 3 * i] = (int32_t)cy;
     }
     Py_DECREF(rs);
-    return PyLong_FromSsize_t(2 + 3 * A);
+    return 2 + 3 * A;
+}
+
+/* pack_robots(addr, cap_words, t, robots) -> words */
+static PyObject* pack_robots(PyObject* self, PyObject* args) {
+    unsigned long long addr;
+    Py_ssize_t cap;
+    long t;
+    PyObject* robots;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "KnlO", &addr, &cap, &t, &robots)) return NULL;
+    const Py_ssize_t nw = do_pack_robots((int32_t*)(uintptr_t)addr, cap, t, robots, -1);
+    return nw < 0 ? NULL : PyLong_FromSsize_t(nw);
+}
+
+/* ---- one-call helpers ---- */
+typedef int (*views_features_fn)(void* eng, const int32_t* views, const int64_t* offsets, int32_t n_views,
+                                 int32_t max_slots, const int32_t* agent_idx, int32_t T, int32_t MO, int32_t MP,
+                                 int32_t MR, int32_t MPs, float* obs, float* vec, float* gmap, float* gvec,
+                                 void* stream);
+typedef int (*views_shaped_fn)(void* eng, const int32_t* prev_views, const int64_t* prev_offsets, int32_t max_slots,
+                               const int32_t* cur, const int64_t* cur_offsets, const uint8_t* actions,
+                               const int64_t* act_offsets, const double* g, int32_t n, const double* consts,
+                               float* out, void* stream);
+typedef int (*view_features_fn)(void* eng, const int32_t* rec, int32_t words, int32_t agent_index, int32_t T,
+                                int32_t MO, int32_t MP, int32_t MR, int32_t MPs, float* obs, float* vec, float* gmap,
+                                float* gvec, void* stream);
+typedef int (*view_shaped_fn)(void* eng, const int32_t* prev_view, int32_t prev_words, const int32_t* cur,
+                              int32_t cur_words, const uint8_t* actions, int32_t n_actions, double g,
+                              const double* consts, float* out, void* stream);
+typedef const char* (*last_error_fn)(void);
+static views_features_fn f_features;
+static views_shaped_fn f_shaped;
+static view_features_fn f_features1;
+static view_shaped_fn f_shaped1;
+static last_error_fn f_last_error;
+static PyObject* exc_type;   /* marl_gpu._lib.MdlError */
+
+/* bind(addr mdl_host_views_features, addr mdl_host_views_shaped_reward, addr mdl_host_view_features,
+ *      addr mdl_host_view_shaped_reward, addr mdl_last_error, MdlError) */
+static PyObject* bind(PyObject* self, PyObject* args) {
+    unsigned long long a, b, a1, b1, c;
+    PyObject* exc;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "KKKKKO", &a, &b, &a1, &b1, &c, &exc)) return NULL;
+    f_features = (views_features_fn)(uintptr_t)a;
+    f_shaped = (views_shaped_fn)(uintptr_t)b;
+    f_features1 = (view_features_fn)(uintptr_t)a1;
+    f_shaped1 = (view_shaped_fn)(uintptr_t)b1;
+    f_last_error = (last_error_fn)(uintptr_t)c;
+    Py_INCREF(exc);
+    Py_XSETREF(exc_type, exc);
+    Py_RETURN_NONE;
+}
+
+static PyObject* lib_error(const char* what) {
+    PyErr_Format(exc_type ? exc_type : PyExc_RuntimeError, "%s: %s", what, f_last_error ? f_last_error() : "?");
+    return NULL;
+}
+
+static Py_ssize_t align16(Py_ssize_t x) { return (x + 15) & ~(Py_ssize_t)15; }
+
+static Py_ssize_t seq_len(PyObject* o) {
+    if (PyDict_Check(o)) return PyDict_Size(o);
+    return PyObject_Length(o);
+}
+
+/* features(eng, stream, arena, cap_bytes, t, robots, tracker, H, W, agent_index, T, MO, MP, MR, MPs, want)
+ *   -> tuple of float32 arrays for the bits of `want` (1 obs [6,H,W], 2 vec [6+5MO+5MP+1],
+ *      4 gmap [4,H,W], 8 gvec [6MR+7MPs+1]), or the arena bytes needed (int) when cap_bytes is short.
+ * A record of at most MDL_VIEW_INLINE_WORDS words travels in the kernel arguments
+ * (mdl_host_view_features) and the arena holds only the outputs; a larger one goes through the
+ * arena: view record | int64 offset 0 | agent index | outputs (16-byte aligned). */
+static PyObject* features(PyObject* self, PyObject* args) {
+    unsigned long long eng, stream, arena;
+    Py_ssize_t cap;
+    long t, H, W, idx, T, MO, MP, MR, MPs, want;
+    PyObject *robots, *tracker;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "KKKnlOOlllllllll", &eng, &stream, &arena, &cap, &t, &robots, &tracker, &H, &W, &idx,
+                          &T, &MO, &MP, &MR, &MPs, &want))
+        return NULL;
+    if (!f_features) {
+        PyErr_SetString(PyExc_RuntimeError, "_mdl_pack.bind() not called");
+        return NULL;
+    }
+    const Py_ssize_t A = seq_len(robots), ns = seq_len(tracker);
+    if (A < 0 || ns < 0) return NULL;
+    const Py_ssize_t HW = H * W;
+    const Py_ssize_t sz[4] = {6 * HW, 6 + 5 * MO + 5 * MP + 1, 4 * HW, 6 * MR + 7 * MPs + 1};
+    const Py_ssize_t vw = 4 + 3 * A + 8 * ns;
+    const int inl = vw <= MDL_VIEW_INLINE_WORDS;
+    const Py_ssize_t o_off = align16(4 * vw), o_idx = align16(o_off + 8);
+    Py_ssize_t pos = inl ? 0 : align16(o_idx + 4), o_out[4];
+    int nout = 0;
+    for (int k = 0; k < 4; k++) {
+        o_out[k] = -1;
+        if (want & (1 << k)) {
+            o_out[k] = pos;
+            pos = align16(pos + 4 * sz[k]);
+            nout++;
+        }
+    }
+    if (pos > cap) return PyLong_FromSsize_t(pos);
+    char* b = (char*)(uintptr_t)arena;
+    float* outp[4];
+    for (int k = 0; k < 4; k++) outp[k] = o_out[k] >= 0 ? (float*)(b + o_out[k]) : NULL;
+    int rc;
+    if (inl) {
+        int32_t rec[MDL_VIEW_INLINE_WORDS];
+        if (do_pack_view(rec, vw, t, robots, tracker, H, W, 0, -1) < 0) return NULL;
+        Py_BEGIN_ALLOW_THREADS
+        rc = f_features1((void*)(uintptr_t)eng, rec, (int32_t)vw, (int32_t)idx, (int32_t)T, (int32_t)MO, (int32_t)MP,
+                         (int32_t)MR, (int32_t)MPs, outp[0], outp[1], outp[2], outp[3], (void*)(uintptr_t)stream);
+        Py_END_ALLOW_THREADS
+        if (rc) return lib_error("mdl_host_view_features");
+    } else {
+        if (do_pack_view((int32_t*)b, vw, t, robots, tracker, H, W, 0, -1) < 0) return NULL;
+        *(int64_t*)(b + o_off) = 0;
+        *(int32_t*)(b + o_idx) = (int32_t)idx;
+        Py_BEGIN_ALLOW_THREADS
+        rc = f_features((void*)(uintptr_t)eng, (const int32_t*)b, (const int64_t*)(b + o_off), 1, (int32_t)ns,
+                        (const int32_t*)(b + o_idx), (int32_t)T, (int32_t)MO, (int32_t)MP, (int32_t)MR, (int32_t)MPs,
+                        outp[0], outp[1], outp[2], outp[3], (void*)(uintptr_t)stream);
+        Py_END_ALLOW_THREADS
+        if (rc) return lib_error("mdl_host_views_features");
+    }
+    PyObject* tup = PyTuple_New(nout);
+    if (!tup) return NULL;
+    int j = 0;
+    for (int k = 0; k < 4; k++) {
+        if (!outp[k]) continue;
+        npy_intp dims[3] = {k == 0 ? 6 : 4, H, W};
+        if (k == 1 || k == 3) dims[0] = sz[k];
+        PyObject* arr = PyArray_SimpleNew((k == 1 || k == 3) ? 1 : 3, dims, NPY_FLOAT32);
+        if (!arr) {
+            Py_DECREF(tup);
+            return NULL;
+        }
+        memcpy(PyArray_DATA((PyArrayObject*)arr), outp[k], 4 * (size_t)sz[k]);
+        PyTuple_SET_ITEM(tup, j++, arr);
+    }
+    return tup;
+}
+
+/* MOVE_CODES / OP_CODES of marl_gpu.compat: one-character strings, anything else 5 / 3 */
+static int move_code(PyObject* o) {
+    if (PyUnicode_Check(o) && PyUnicode_GET_LENGTH(o) == 1) {
+        switch (PyUnicode_READ_CHAR(o, 0)) {
+            case 'S': return 0;
+            case 'L': return 1;
+            case 'R': return 2;
+            case 'U': return 3;
+            case 'D': return 4;
+        }
+    }
+    return 5;
+}
+
+static int op_code(PyObject* o) {
+    if (PyUnicode_Check(o) && PyUnicode_GET_LENGTH(o) == 1) {
+        const Py_UCS4 c = PyUnicode_READ_CHAR(o, 0);
+        if (c >= '0' && c <= '2') return (int)(c - '0');
+    }
+    return 3;
+}
+
+/* shaped(eng, stream, arena, cap_bytes, g, prev_t, prev_robots, cur_t, cur_robots, actions, num_agents, tracker,
+ *        H, W, consts_addr) -> numpy.float32, or the arena bytes needed (int) when cap_bytes is short.
+ * actions: (move, op) pairs (compat._code's mapping) or bytes of MDL_ACTION_CODES.
+ * The first num_agents robots / actions of each (list(...)[:num_agents], MAPPO/helper.py:257-369).
+ * Arena layout: prev view | cur record | action codes | int64 offset 0 | pad | g (f64) | out (f32). */
+static PyObject* shaped(PyObject* self, PyObject* args) {
+    unsigned long long eng, stream, arena, consts;
+    Py_ssize_t cap, na;
+    double g;
+    long pt, ct, H, W;
+    PyObject *prev_r, *cur_r, *actions, *tracker;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "KKKndlOlOOnOllK", &eng, &stream, &arena, &cap, &g, &pt, &prev_r, &ct, &cur_r,
+                          &actions, &na, &tracker, &H, &W, &consts))
+        return NULL;
+    if (!f_shaped) {
+        PyErr_SetString(PyExc_RuntimeError, "_mdl_pack.bind() not called");
+        return NULL;
+    }
+    Py_ssize_t Ap = seq_len(prev_r), Ac = seq_len(cur_r), ns = seq_len(tracker);
+    if (Ap < 0 || Ac < 0 || ns < 0) return NULL;
+    /* (move, op) pairs, or code bytes (MDL_ACTION_CODES) */
+    const int as_codes = PyBytes_Check(actions);
+    PyObject* acts = as_codes ? (Py_INCREF(actions), actions) : PySequence_Fast(actions, "actions must be a sequence");
+    if (!acts) return NULL;
+    Py_ssize_t Na = as_codes ? PyBytes_GET_SIZE(acts) : PySequence_Fast_GET_SIZE(acts);
+    /* Python's [:num_agents] */
+    const Py_ssize_t lim_p = na >= 0 ? na : Ap + na, lim_c = na >= 0 ? na : Ac + na, lim_a = na >= 0 ? na : Na + na;
+    Ap = lim_p < 0 ? 0 : (lim_p < Ap ? lim_p : Ap);
+    Ac = lim_c < 0 ? 0 : (lim_c < Ac ? lim_c : Ac);
+    Na = lim_a < 0 ? 0 : (lim_a < Na ? lim_a : Na);
+    const Py_ssize_t vw = 4 + 3 * Ap + 8 * ns, cw = 2 + 3 * Ac;
+    /* inline (mdl_host_view_shaped_reward): the inputs in the kernel arguments, the output at arena
+     * offset 0; else the arena layout above */
+    const int inl = vw + cw + (Na + 3) / 4 <= MDL_VIEW_INLINE_WORDS;
+    const Py_ssize_t o_c = align16(4 * vw), o_a = align16(o_c + 4 * cw), o_off = align16(o_a + Na);
+    const Py_ssize_t o_out = inl ? 0 : o_off + 24, need = inl ? 16 : o_off + 48;
+    int32_t rec[MDL_VIEW_INLINE_WORDS];
+    PyObject* ret = NULL;
+    if (Na < Ap || Ac < Ap) {   /* the reference indexes all three per agent (IndexError) */
+        PyErr_Format(PyExc_IndexError, "%zd robots before the step, but %zd after and %zd actions", Ap, Ac, Na);
+        goto done;
+    }
+    if (need > cap) {
+        ret = PyLong_FromSsize_t(need);
+        goto done;
+    }
+    char* b = (char*)(uintptr_t)arena;
+    char* in = inl ? (char*)rec : b;   /* where the inputs are packed */
+    const Py_ssize_t i_c = inl ? 4 * vw : o_c, i_a = inl ? 4 * (vw + cw) : o_a;
+    if (do_pack_view((int32_t*)in, vw, pt, prev_r, tracker, H, W, 0, Ap) < 0) goto done;
+    if (do_pack_robots((int32_t*)(in + i_c), cw, ct, cur_r, Ac) < 0) goto done;
+    if (as_codes) memcpy(in + i_a, PyBytes_AS_STRING(acts), (size_t)Na);
+    for (Py_ssize_t i = 0; i < Na && !as_codes; i++) {
+        PyObject* pr = PySequence_Fast(PySequence_Fast_GET_ITEM(acts, i), "each action must be a (move, op) pair");
+        if (!pr) goto done;
+        if (PySequence_Fast_GET_SIZE(pr) != 2) {
+            Py_DECREF(pr);
+            PyErr_SetString(PyExc_ValueError, "each action must be a (move, op) pair");
+            goto done;
+        }
+        in[i_a + i] = (char)(move_code(PySequence_Fast_GET_ITEM(pr, 0)) | (op_code(PySequence_Fast_GET_ITEM(pr, 1)) << 3));
+        Py_DECREF(pr);
+    }
+    int rc;
+    const double* cp = consts ? (const double*)(uintptr_t)consts : NULL;
+    if (inl) {
+        Py_BEGIN_ALLOW_THREADS
+        rc = f_shaped1((void*)(uintptr_t)eng, rec, (int32_t)vw, rec + vw, (int32_t)cw, (const uint8_t*)(rec + vw + cw),
+                       (int32_t)Na, g, cp, (float*)(b + o_out), (void*)(uintptr_t)stream);
+        Py_END_ALLOW_THREADS
+    } else {
+        *(int64_t*)(b + o_off) = 0;
+        *(int64_t*)(b + o_off + 8) = 0;
+        *(double*)(b + o_off + 16) = g;
+        Py_BEGIN_ALLOW_THREADS
+        rc = f_shaped((void*)(uintptr_t)eng, (const int32_t*)b, (const int64_t*)(b + o_off), (int32_t)ns,
+                      (const int32_t*)(b + o_c), (const int64_t*)(b + o_off), (const uint8_t*)(b + o_a),
+                      (const int64_t*)(b + o_off), (const double*)(b + o_off + 16), 1, cp, (float*)(b + o_out),
+                      (void*)(uintptr_t)stream);
+        Py_END_ALLOW_THREADS
+    }
+    if (rc) {
+        lib_error(inl ? "mdl_host_view_shaped_reward" : "mdl_host_views_shaped_reward");
+        goto done;
+    }
+    ret = PyArrayScalar_New(Float);
+    if (ret) PyArrayScalar_ASSIGN(ret, Float, *(const float*)(b + o_out));
+done:
+    Py_DECREF(acts);
+    return ret;
 }
 
 static PyMethodDef methods[] = {
     {"pack_view", pack_view, METH_VARARGS, "Pack a state view record into host memory; returns words written."},
     {"pack_robots", pack_robots, METH_VARARGS, "Pack a [t, A, robots] record into host memory."},
+    {"bind", bind, METH_VARARGS, "Bind the engine's self-publishing helper entry points."},
+    {"features", features, METH_VARARGS, "One helper featurizer call: pack, launch, wait, numpy outputs."},
+    {"shaped", shaped, METH_VARARGS, "One compute_shaped_rewards call: pack, launch, wait, numpy.float32."},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_mdl_pack", NULL, -1, methods, NULL, NULL, NULL, NULL};
 
 PyMODINIT_FUNC PyInit__mdl_pack(void) {
+    import_array();
     s_in_transit = PyUnicode_InternFromString("in_transit");
     k_id = PyUnicode_InternFromString("id");
     k_status = PyUnicode_InternFromString("status");

@@ -88,6 +88,12 @@ SIGNATURES = {
     "mdl_views_features": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32,
                                      _vp, _vp, _vp, _vp, _vp]),
     "mdl_views_shaped_reward": (C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "mdl_host_views_features": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32,
+                                          _vp, _vp, _vp, _vp, _vp]),
+    "mdl_host_views_shaped_reward": (C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "mdl_host_view_features": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
+                                         _vp]),
+    "mdl_host_view_shaped_reward": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, C.c_double, _vp, _vp, _vp]),
     "mdl_rank_table": (C.c_int, [_i32, _i32, _vp]),
     "mdl_get_config": (C.c_int, [_vp, C.POINTER(MdlConfig)]),
     "mdl_obs_dims": (C.c_int, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

@@ -14,7 +14,6 @@ import numpy as np
 
 from . import _mdl_pack
 from ._lib import check, lib
-from ._lib import raw_stream as _raw_stream
 from .helper import _align, _arena, _engine_for, _tracker_rows
 
 OP_NO_MATCH = 255   # a string op: the reference compares it with the ints 1 / 2 and never matches
@@ -49,7 +48,7 @@ def _alt(state, persistent_packages, agent_indices, shape, want):
     check(lib().mdl_views_alt_features(eng._h, b, b + o_off, n, ns, b + o_idx,
                                        b + o_out["idq"] if "idq" in o_out else None,
                                        b + o_out["qmix"] if "qmix" in o_out else None, int(oh), int(ow),
-                                       _raw_stream(ar._dev)), "mdl_views_alt_features")
+                                       ar.stream), "mdl_views_alt_features")
     ar.wait()
     shapes = {"idq": (n, 6, H, W), "qmix": (n, 7, oh, ow)}
     res = {k: u8[o_out[k]:o_out[k] + 4 * n * sizes[k]].view(np.float32).reshape(shapes[k]).copy() for k in names}
@@ -108,6 +107,6 @@ def reward_shaping(prev_env_state, current_env_state, actions_taken, persistent_
     u8[o_a:o_a + len(ops)] = np.frombuffer(ops, np.uint8)
     u8[o_off:o_off + 32] = 0
     check(lib().mdl_views_idq_reward(eng._h, b, b + o_off, ns, b + o_c, b + o_off, b + o_a, b + o_off, 1, 1,
-                                     b + o_out, _raw_stream(ar._dev)), "mdl_views_idq_reward")
+                                     b + o_out, ar.stream), "mdl_views_idq_reward")
     ar.wait()
     return [float(v) for v in u8[o_out:o_out + 8 * num_agents].view(np.float64)]

@@ -9,25 +9,26 @@ generate_vector_features):
   convert_global_state(state, tracker, T, MR=100, MPs=100)         -> (f32[4,H,W], f32[Dg])  :167-255
   compute_shaped_rewards(g, prev, cur, actions, tracker_prev, A)   -> np.float32   :257-369
 
-Each call packs the dict(s) into the engine's view record format straight into
-the engine's host-mapped arena (a C extension walks the dicts: _mdl_pack), runs
-the same device code the batched engine uses (mdl_views_features /
-mdl_views_shaped_reward) reading its inputs from and writing its outputs to
-that host memory, and waits for a completion word (mdl_host_wait): one kernel
-launch plus a one-wave publish, no copies and no stream synchronisation.
+Each call is one C call (_mdl_pack.features / .shaped): it packs the dict(s)
+into the engine's view record format straight into the engine's host-mapped
+arena, launches the same device code the batched engine uses
+(mdl_host_views_features / mdl_host_views_shaped_reward: mdl_views_* reading
+their inputs from and writing their outputs to that host memory, whose last
+wave publishes a completion word), spins on that word and returns the numpy
+result: one kernel launch, no copies, no stream synchronisation, no ctypes.
+The launches go to a helper stream of the engine's own (nothing on the device
+depends on them), so they never queue behind the caller's GPU work.
 They exist for drop-in use and for the known-answer tests; batched training
 should use BatchedEnv.build_obs instead.
 """
 from __future__ import annotations
 
 import ctypes as C
-import struct
 
 import numpy as np
 
 from . import _mdl_pack
 from ._lib import check, lib
-from ._lib import raw_stream as _raw_stream
 from .engine import MAPPO_SHAPING, QMIX_SHAPING, BatchedEnv
 from .compat import MOVE_CODES, OP_CODES, _code  # noqa: F401  (MOVE_CODES / OP_CODES re-exported)
 
@@ -35,13 +36,13 @@ _engines: dict = {}
 _CONSTS: dict = {}   # shaping-constant tuples -> their C double[9]
 
 
-_last_grid: list = [None, None]   # [grid object, engine] of the previous call
+_last_grid: list = [None, None]   # [grid object, _Arena] of the previous call
 
 
-def _engine_for(grid) -> BatchedEnv:
-    """The helper engine of a map.  The reference's state dicts carry the env's own grid object
-    (``state['map']`` aliases ``env.grid``, env.py:140), so the same object is recognised by
-    identity first; any other grid is keyed by its contents."""
+def _arena_for(grid) -> "_Arena":
+    """The helper engine of a map, as its arena.  The reference's state dicts carry the env's own
+    grid object (``state['map']`` aliases ``env.grid``, env.py:140), so the same object is
+    recognised by identity first; any other grid is keyed by its contents."""
     if grid is _last_grid[0]:
         return _last_grid[1]
     g = np.asarray(grid, dtype=np.uint8)
@@ -50,22 +51,50 @@ def _engine_for(grid) -> BatchedEnv:
     if eng is None:
         eng = BatchedEnv(g, 1, 1, 1, 2, tracker="fresh")
         _engines[key] = eng
-    _last_grid[0], _last_grid[1] = grid, eng
-    return eng
+    ar = _arena(eng)
+    _last_grid[0], _last_grid[1] = grid, ar
+    return ar
+
+
+def _engine_for(grid) -> BatchedEnv:
+    return _arena_for(grid).eng
+
+
+_bound: list = [False]
+
+
+def _bind():
+    """Hand the C packer the engine's self-publishing helper entries (once)."""
+    if not _bound[0]:
+        from ._lib import MdlError
+        L = lib()
+        addr = lambda f: C.cast(f, C.c_void_p).value  # noqa: E731
+        _mdl_pack.bind(addr(L.mdl_host_views_features), addr(L.mdl_host_views_shaped_reward),
+                       addr(L.mdl_host_view_features), addr(L.mdl_host_view_shaped_reward),
+                       addr(L.mdl_last_error), MdlError)
+        _bound[0] = True
 
 
 class _Arena:
     """The engine's host-mapped arena (mdl_host_arena) as one numpy byte view; grows on demand
-    (every call has finished with it on return: mdl_host_wait is synchronous)."""
+    (every call has finished with it on return: the helper calls are synchronous).  ``h`` /
+    ``stream``: the engine handle and its helper stream, as integers for the C calls."""
 
     def __init__(self, eng):
+        import torch
+        _bind()
         self.eng = eng
         self.cap = 0
         self.addr = 0
         self.u8 = None
         L = lib()
-        self._views, self._shaped, self._wait = L.mdl_views_features, L.mdl_views_shaped_reward, L.mdl_host_wait
+        self._views, self._wait = L.mdl_host_views_features, L.mdl_host_wait
         self._dev = eng.device.index
+        self._stream_obj = torch.cuda.Stream(device=eng.device)
+        self.stream = int(self._stream_obj.cuda_stream)
+        self.h = int(eng._h.value if isinstance(eng._h, C.c_void_p) else eng._h)
+        self.hw = tuple(int(x) for x in eng.grids[0].shape)
+        self.get(1)
 
     def get(self, nbytes):
         if nbytes > self.cap:
@@ -79,7 +108,7 @@ class _Arena:
         return self.u8
 
     def wait(self):
-        rc = self._wait(self.eng._h, _raw_stream(self._dev))
+        rc = self._wait(self.eng._h, self.stream)
         if rc:
             check(rc, "mdl_host_wait")
 
@@ -138,20 +167,35 @@ def _features_layout(H, W, A, ns, n, MO, MP, MR, MPs, want):
     return lay
 
 
+def _one(state, tracker, idx, T, MO, MP, MR, MPs, want):
+    """One view (one C call): the outputs named by the bits of ``want`` (1 obs, 2 vec, 4 gmap, 8 gvec)."""
+    grid = state["map"]
+    ar = _last_grid[1] if grid is _last_grid[0] else _arena_for(grid)
+    H, W = ar.hw
+    T = int(T)
+    r = _mdl_pack.features(ar.h, ar.stream, ar.addr, ar.cap, state["time_step"], state["robots"], tracker, H, W, idx,
+                           T, MO, MP, MR, MPs, want)
+    if r.__class__ is int:   # the arena is too small for this call: grow it, once
+        ar.get(r)
+        r = _mdl_pack.features(ar.h, ar.stream, ar.addr, ar.cap, state["time_step"], state["robots"], tracker, H, W,
+                               idx, T, MO, MP, MR, MPs, want)
+    return r
+
+
 def features(state, tracker, agent_indices, T, MO, MP, MR, MPs, want=("obs", "vec", "gmap", "gvec")):
     """Batched helper entry: one view per agent index (same state / tracker: one record that
     every view's offset points at).  ``tracker``: the reference's tracker dict (insertion order)
     or rows (id, status 1|2, sr, sc, tr, tc, start_time, deadline)."""
     grid = state["map"]
-    eng = _engine_for(grid)
-    H, W = len(grid), len(grid[0])
+    ar = _arena_for(grid)
+    eng = ar.eng
+    H, W = ar.hw
     if not isinstance(tracker, dict):
         tracker = np.asarray(tracker, np.int64).reshape(-1, 8).tolist()
     robots = state["robots"]
     ns = len(tracker)
     n = len(agent_indices)
     vw, o_off, o_idx, nbytes, outs, o_ptr = _features_layout(H, W, len(robots), ns, n, MO, MP, MR, MPs, tuple(want))
-    ar = eng.__dict__.get("_arena") or _arena(eng)
     u8 = ar.get(nbytes)
     base = ar.addr
     _mdl_pack.pack_view(base, vw, int(state["time_step"]), robots, tracker, H, W, 0)
@@ -160,70 +204,67 @@ def features(state, tracker, agent_indices, T, MO, MP, MR, MPs, want=("obs", "ve
     rc = ar._views(eng._h, base, base + o_off, n, ns, base + o_idx, int(T), MO, MP, MR, MPs,
                    None if o_ptr[0] is None else base + o_ptr[0], None if o_ptr[1] is None else base + o_ptr[1],
                    None if o_ptr[2] is None else base + o_ptr[2], None if o_ptr[3] is None else base + o_ptr[3],
-                   _raw_stream(ar._dev))
+                   ar.stream)
     if rc:
-        check(rc, "mdl_views_features")
-    ar.wait()
+        check(rc, "mdl_host_views_features")
     return {k: u8[o:o + nb].view(np.float32).reshape(shape).copy() for k, (o, nb, shape) in outs.items()}
 
 
 def convert_observation(env_state_dict, persistent_packages_for_env, current_robot_idx):
-    return features(env_state_dict, persistent_packages_for_env, [current_robot_idx], 0, 0, 0, 0, 0,
-                    want=("obs",))["obs"][0]
+    return _one(env_state_dict, persistent_packages_for_env, current_robot_idx, 0, 0, 0, 0, 0, 1)[0]
 
 
 def generate_vector_features(env_state_dict, persistent_packages_for_env, current_robot_idx, max_time_steps,
                              max_other_robots_to_observe=100, max_packages_to_observe=100):
-    return features(env_state_dict, persistent_packages_for_env, [current_robot_idx], max_time_steps,
-                    max_other_robots_to_observe, max_packages_to_observe, 0, 0, want=("vec",))["vec"][0]
+    return _one(env_state_dict, persistent_packages_for_env, current_robot_idx, max_time_steps,
+                max_other_robots_to_observe, max_packages_to_observe, 0, 0, 2)[0]
 
 
 def convert_global_state(env_state_dict, persistent_packages_for_env, max_time_steps, max_robots_in_state=100,
                          max_packages_in_state=100):
-    o = features(env_state_dict, persistent_packages_for_env, [0], max_time_steps, 0, 0, max_robots_in_state,
-                 max_packages_in_state, want=("gmap", "gvec"))
-    return o["gmap"][0], o["gvec"][0]
+    return _one(env_state_dict, persistent_packages_for_env, 0, max_time_steps, 0, 0, max_robots_in_state,
+                max_packages_in_state, 12)
+
+
+_last_consts: list = [None, 0]   # [constants tuple, address of its C double[9]] of the previous call
+
+
+def _consts_addr(consts):
+    """Address of a C double[9] holding ``consts`` (0: the engine's own); cached per tuple."""
+    if consts is None:
+        return 0
+    if consts is _last_consts[0]:
+        return _last_consts[1]
+    ck = tuple(consts)
+    cs = _CONSTS.get(ck)
+    if cs is None:
+        cs = _CONSTS[ck] = (C.c_double * 9)(*[float(v) for v in ck])
+    a = C.addressof(cs)
+    if isinstance(consts, tuple):   # immutable: safe to recognise by identity next time
+        _last_consts[0], _last_consts[1] = consts, a
+    return a
+
+
+def _shaped(ar, g, prev_t, prev_robots1, cur_t, cur_robots1, actions, num_agents, tracker, consts):
+    """One transition (one C call).  ``actions``: (move, op) pairs, or MDL_ACTION_CODES bytes."""
+    H, W = ar.hw
+    ca = _consts_addr(consts)
+    r = _mdl_pack.shaped(ar.h, ar.stream, ar.addr, ar.cap, g, prev_t, prev_robots1, cur_t, cur_robots1, actions,
+                         num_agents, tracker, H, W, ca)
+    if r.__class__ is int:   # the arena is too small for this call: grow it, once
+        ar.get(r)
+        r = _mdl_pack.shaped(ar.h, ar.stream, ar.addr, ar.cap, g, prev_t, prev_robots1, cur_t, cur_robots1, actions,
+                             num_agents, tracker, H, W, ca)
+    return r
 
 
 def shaped_rewards_views(g, prev_t, prev_robots1, cur_t, cur_robots1, action_codes, tracker, grid,
                          consts=MAPPO_SHAPING):
-    """Raw entry for compute_shaped_rewards: one transition; ``tracker``: the tracker dict of the
-    previous state (insertion order) or its rows."""
-    eng = _engine_for(grid)
-    H, W = len(grid), len(grid[0])
-    if not isinstance(tracker, dict):
-        tracker = np.asarray(tracker, np.int64).reshape(-1, 8).tolist()
-    ns = len(tracker)
-    codes = bytes(action_codes)
-    key = (len(prev_robots1), ns, len(cur_robots1), len(codes))
-    lay = _layouts.get(key)
-    if lay is None:   # arena: prev view | cur record | action bytes | three int64 offsets (0) | g (f64) | out (f32)
-        vw = 4 + 3 * key[0] + 8 * ns
-        cw = 2 + 3 * key[2]
-        o_c = _align(4 * vw)
-        o_a = _align(o_c + 4 * cw)
-        o_off = _align(o_a + key[3])
-        lay = _layouts[key] = (vw, cw, o_c, o_a, o_off, o_off + 24, o_off + 48)
-    vw, cw, o_c, o_a, o_off, o_out, nbytes = lay
-    ar = eng.__dict__.get("_arena") or _arena(eng)
-    u8 = ar.get(nbytes)
-    b = ar.addr
-    _mdl_pack.pack_view(b, vw, int(prev_t), prev_robots1, tracker, H, W, 0)
-    _mdl_pack.pack_robots(b + o_c, cw, int(cur_t), cur_robots1)
-    u8[o_a:o_a + len(codes)] = np.frombuffer(codes, np.uint8)
-    struct.pack_into("<qqd", u8, o_off, 0, 0, float(g))   # the offsets (all 0) and g
-    cs = None
-    if consts is not None:
-        ck = tuple(consts)
-        cs = _CONSTS.get(ck)
-        if cs is None:
-            cs = _CONSTS[ck] = (C.c_double * 9)(*[float(v) for v in consts])
-    rc = ar._shaped(eng._h, b, b + o_off, ns, b + o_c, b + o_off, b + o_a, b + o_off, b + o_off + 16, 1, cs,
-                    b + o_out, _raw_stream(ar._dev))
-    if rc:
-        check(rc, "mdl_views_shaped_reward")
-    ar.wait()
-    return np.float32(struct.unpack_from("<f", u8, o_out)[0])
+    """Raw entry for compute_shaped_rewards: one transition; ``action_codes``: MDL_ACTION_CODES
+    bytes (move | op << 3); ``tracker``: the tracker dict of the previous state (insertion order)
+    or its rows."""
+    return _shaped(_arena_for(grid), float(g), int(prev_t), prev_robots1, int(cur_t), cur_robots1,
+                   bytes(action_codes), len(prev_robots1), tracker, consts)
 
 
 def compute_shaped_rewards(global_reward, prev_env_state_dict, current_env_state_dict, actions_taken_for_all_agents,
@@ -232,20 +273,21 @@ def compute_shaped_rewards(global_reward, prev_env_state_dict, current_env_state
 
     The state dicts need no 'map' key (the notebook KAT omits it); ``grid``
     defaults to a map large enough for the coordinates used."""
-    prev_r = list(prev_env_state_dict["robots"])[:num_agents]
-    cur_r = list(current_env_state_dict["robots"])[:num_agents]
-    codes = bytes([_code(m, o) for m, o in list(actions_taken_for_all_agents)[:num_agents]])
-    trk = persistent_packages_at_prev_state
     if grid is None:
         grid = prev_env_state_dict.get("map")
     if grid is None:
+        trk = persistent_packages_at_prev_state
+        prev_r = list(prev_env_state_dict["robots"])[:num_agents]
+        cur_r = list(current_env_state_dict["robots"])[:num_agents]
         rows = _tracker_rows(trk) if isinstance(trk, dict) else np.asarray(trk).reshape(-1, 8)
         coords = [x for r in prev_r + cur_r for x in r[:2]]
         coords += [int(v) + 1 for row in rows for v in row[2:6]]
         n = max(coords + [2])
         grid = [[0] * n for _ in range(n)]
-    return shaped_rewards_views(global_reward, prev_env_state_dict["time_step"], prev_r,
-                                current_env_state_dict["time_step"], cur_r, codes, trk, grid, consts)
+    ar = _last_grid[1] if grid is _last_grid[0] else _arena_for(grid)
+    return _shaped(ar, global_reward, prev_env_state_dict["time_step"], prev_env_state_dict["robots"],
+                   current_env_state_dict["time_step"], current_env_state_dict["robots"],
+                   actions_taken_for_all_agents, num_agents, persistent_packages_at_prev_state, consts)
 
 
 __all__ = ["convert_observation", "generate_vector_features", "convert_global_state", "compute_shaped_rewards",

@@ -178,6 +178,36 @@ def test_helper_dict_cases_golden():
             assert sh.tobytes() == d[f"sh_{i}"][j].tobytes(), (i, c, j)
 
 
+def test_helper_public_functions_golden():
+    """The reference-signature helpers (one C call each: pack, launch, wait), with the tracker as the
+    reference's dict and the actions as (move, op) string pairs, against the same fixtures."""
+    from marl_gpu import helper as Hm
+    d = npz("helpers.npz")
+    mv_s, op_s = ["S", "L", "R", "U", "D", "X"], ["0", "1", "2", "9"]
+    for i, c in enumerate(meta(d)):
+        g = grid(c["map"]).tolist()
+        rows = d[f"trk_{i}"].tolist()
+        trk = {r[0]: {"id": r[0], "status": "in_transit" if r[1] == 2 else "waiting", "start_pos": (r[2], r[3]),
+                      "target_pos": (r[4], r[5]), "start_time": r[6], "deadline": r[7]} for r in rows}
+        robots = [tuple(x) for x in d[f"robots_{i}"].tolist()]
+        state = {"time_step": c["t"], "map": g, "robots": robots, "packages": []}
+        for tk in (trk, rows):
+            o = Hm.convert_observation(state, tk, c["idx"])
+            assert o.shape == d[f"obs_{i}"].shape
+            np.testing.assert_array_equal(o, d[f"obs_{i}"], err_msg=str(c))
+            v = Hm.generate_vector_features(state, tk, c["idx"], c["T"], c["MO"], c["MP"])
+            np.testing.assert_array_equal(v, d[f"vec_{i}"], err_msg=str(c))
+            gm, gv = Hm.convert_global_state(state, tk, c["T"], c["MR"], c["MPs"])
+            np.testing.assert_array_equal(gm, d[f"gmap_{i}"], err_msg=str(c))
+            np.testing.assert_array_equal(gv, d[f"gvec_{i}"], err_msg=str(c))
+        acts = [(mv_s[a], op_s[b]) for a, b in d[f"acts_{i}"].tolist()]
+        cur = {"time_step": c["t"] + 1, "map": g, "robots": [tuple(x) for x in d[f"cur_robots_{i}"].tolist()]}
+        g0 = 0 if c["g_int"] else c["g"]
+        for j, consts in enumerate((Hm.MAPPO_SHAPING, Hm.QMIX_SHAPING)):
+            sh = Hm.compute_shaped_rewards(g0, state, cur, acts, trk, len(robots), consts=consts)
+            assert isinstance(sh, np.float32) and sh.tobytes() == d[f"sh_{i}"][j].tobytes(), (i, c, j)
+
+
 def test_notebook_kat():
     from marl_gpu import helper as Hm
     k = load_json("kat.json")

@@ -74,11 +74,33 @@ int main() {
                     CK(hipEventElapsedTime(&ms, e0, e1));
                     ev.push_back(ms * 1e3);
                 }
+                // the same N launches issued one by one from this host loop (no graph)
+                std::vector<double> wall2, ev2;
+                for (int r = 0; r < 30; r++) {
+                    for (int i = 0; i < 5; i++) hipLaunchKernelGGL(k_small, dim3(256), dim3(1024), 0, s, sink, ticks);
+                    CK(hipStreamSynchronize(s));
+                    const double t0 = now_us();
+                    CK(hipEventRecord(e0, s));
+                    for (int i = 0; i < N; i++) {
+                        if (big) hipLaunchKernelGGL(k_big, dim3(256), dim3(1024), 0, s, b, sink, ticks);
+                        else hipLaunchKernelGGL(k_small, dim3(256), dim3(1024), 0, s, sink, ticks);
+                    }
+                    CK(hipEventRecord(e1, s));
+                    CK(hipStreamSynchronize(s));
+                    wall2.push_back(now_us() - t0);
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    ev2.push_back(ms * 1e3);
+                }
                 std::sort(wall.begin(), wall.end());
                 std::sort(ev.begin(), ev.end());
+                std::sort(wall2.begin(), wall2.end());
+                std::sort(ev2.begin(), ev2.end());
                 printf("{\"kernarg_bytes\": %d, \"busy_ticks\": %llu, \"nodes\": %d, \"wall_us_median\": %.1f, "
-                       "\"event_us_median\": %.1f, \"wall_us_per_node\": %.2f, \"event_us_per_node\": %.2f}\n",
-                       big ? (int)sizeof(Big) + 16 : 16, ticks, N, wall[15], ev[15], wall[15] / N, ev[15] / N);
+                       "\"event_us_median\": %.1f, \"wall_us_per_node\": %.2f, \"event_us_per_node\": %.2f, "
+                       "\"loop_wall_us_per_launch\": %.2f, \"loop_event_us_per_launch\": %.2f}\n",
+                       big ? (int)sizeof(Big) + 16 : 16, ticks, N, wall[15], ev[15], wall[15] / N, ev[15] / N,
+                       wall2[15] / N, ev2[15] / N);
                 CK(hipGraphExecDestroy(ge));
                 CK(hipGraphDestroy(g));
             }

@@ -208,6 +208,52 @@ def test_helper_public_functions_golden():
             assert isinstance(sh, np.float32) and sh.tobytes() == d[f"sh_{i}"][j].tobytes(), (i, c, j)
 
 
+@pytest.mark.parametrize("mapname,A,ns", [("map1.txt", 5, 20), ("synthetic64.txt", 16, 60), ("map2.txt", 5, 120),
+                                          ("synthetic64.txt", 40, 90)])
+def test_helper_record_size_classes(mapname, A, ns):
+    """The single-view helpers across the record sizes their paths split on: a view record in
+    the small (<= 256 words) or large (<= 768) kernel-argument class, or past it through the
+    arena (mdl_host_views_*), each against the oracle's restatement of MAPPO/helper.py."""
+    from marl_gpu import helper as Hm
+    g = grid(mapname)
+    H, W = g.shape
+    rs = np.random.RandomState(A * 1000 + ns)
+    free = np.argwhere(g == 0)
+    t, T = 37, 100
+    rows = []
+    for k in range(ns):
+        s_, d_ = free[rs.randint(len(free))], free[rs.randint(len(free))]
+        rows.append([k + 1, 2 if k % 4 == 1 else 1, int(s_[0]), int(s_[1]), int(d_[0]), int(d_[1]),
+                     int(rs.randint(0, t + 1)), int(t + rs.randint(-10, 60))])
+    transit = [r[0] for r in rows if r[1] == 2]
+    cells = free[rs.choice(len(free), 2 * A, replace=False)]
+    robots = [(int(cells[i][0]) + 1, int(cells[i][1]) + 1, transit[i] if i < len(transit) and i % 2 else 0)
+              for i in range(A)]
+    cur = [(int(cells[A + i][0]) + 1, int(cells[A + i][1]) + 1, r[2]) for i, r in enumerate(robots)]
+    trk = {r[0]: {"id": r[0], "status": "in_transit" if r[1] == 2 else "waiting", "start_pos": (r[2], r[3]),
+                  "target_pos": (r[4], r[5]), "start_time": r[6], "deadline": r[7]} for r in rows}
+    glist = g.tolist()
+    state = {"time_step": t, "map": glist, "robots": robots, "packages": []}
+    for idx in (0, A - 1):
+        np.testing.assert_array_equal(Hm.convert_observation(state, trk, idx),
+                                      O.convert_observation(g, t, robots, rows, idx))
+        np.testing.assert_array_equal(Hm.generate_vector_features(state, trk, idx, T, 30, 100),
+                                      O.generate_vector_features(H, W, t, robots, rows, idx, T, 30, 100))
+    gm, gv = Hm.convert_global_state(state, trk, T, 50, 120)
+    gm0, gv0 = O.convert_global_state(g, t, robots, rows, T, 50, 120)
+    np.testing.assert_array_equal(gm, gm0)
+    np.testing.assert_array_equal(gv, gv0)
+    mv, op = rs.randint(0, 5, A), rs.randint(0, 3, A)
+    acts = [("SLRUD"[m], "012"[o]) for m, o in zip(mv, op)]
+    curd = {"time_step": t + 1, "map": glist, "robots": cur}
+    for consts, oc in ((Hm.MAPPO_SHAPING, O.MAPPO_CONSTS), (Hm.QMIX_SHAPING, O.QMIX_CONSTS)):
+        sh = Hm.compute_shaped_rewards(1.5, state, curd, acts, trk, A, consts=consts)
+        sh0 = O.compute_shaped_rewards(1.5, t, robots, t + 1, cur, mv, op, rows, A, consts=oc)
+        assert sh.tobytes() == sh0.tobytes(), (consts, float(sh), float(sh0))
+    with pytest.raises(IndexError):   # fewer actions than agents: the reference indexes past them
+        Hm.compute_shaped_rewards(1.5, state, curd, acts[:-1], trk, A)
+
+
 def test_notebook_kat():
     from marl_gpu import helper as Hm
     k = load_json("kat.json")

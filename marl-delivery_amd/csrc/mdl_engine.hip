@@ -641,9 +641,14 @@ int mdl_mail_step(MdlEngine* eng, int32_t n, int32_t use_ids, int32_t auto_reset
     DeviceGuard dg(eng->device);
     hipStream_t s = (hipStream_t)stream;
     const MdlMailbox& m = eng->mbox;
-    HIPCHK(mdl::launch_step(eng->p, m.codes, MDL_ACTION_CODES, use_ids ? m.ids : nullptr, n, auto_reset, m.r_env,
-                            m.r_shaped, m.done, step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, s));
-    return mail_finish(eng, n, use_ids, s, "mdl_mail_step");
+    // one launch: the step, its rows into the mailbox, the completion word (k_step_mail)
+    const int32_t want = eng->mail_seq = (eng->mail_seq % 0x7ffffff0) + 1;
+    const mdl::MailRows rows{m.seq, m.robots, m.pkgs, m.t, m.total_reward, m.rterms};
+    HIPCHK(mdl::launch_step_mail(eng->p, m.codes, use_ids ? m.ids : nullptr, n, auto_reset, m.r_env, m.r_shaped,
+                                 m.done, step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, rows,
+                                 eng->mail_ctr, eng->mail_waves, want, s));
+    eng->mail_waves += (unsigned)n;   // the n waves of rows [0, n) counted themselves
+    return spin_wait(m.seq, want, s, "mdl_mail_step");
 }
 
 int mdl_mail_reset(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream) {

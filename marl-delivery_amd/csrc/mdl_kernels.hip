@@ -375,10 +375,40 @@ struct ObsArgs {
     float* cvec;
 };
 
+// the completion tail of a Publish launch (every wave of the grid runs it, or the `expect`
+// waves that reach it); a one-wave launch (ctr == nullptr) publishes straight after its release
+__device__ __forceinline__ void publish_tail(const Publish& pb) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);   // this wave's stores, before it is counted
+    if (!pb.ctr) {
+        if (lane_id() == 0) __hip_atomic_store(pb.seq, pb.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (lane_id() == 0) {
+        const unsigned waves = pb.expect ? pb.expect : gridDim.x * (blockDim.x / WAVE);
+        if (atomicAdd(pb.ctr, 1u) - pb.base == waves - 1u) {   // the last wave of the grid
+            __atomic_thread_fence(__ATOMIC_ACQ_REL);
+            __hip_atomic_store(pb.seq, pb.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// The dict-API mailbox step's extra arguments (mdl_mail_step): the rows of the envs it steps go
+// straight from the wave's registers into the engine's host-mapped mailbox (k_mail_export's
+// layout), then the launch publishes the call's completion word.  Up to MAIL_INLINE_CODES action
+// bytes travel here in the kernel arguments (no round trip to host memory for them).
+constexpr int MAIL_INLINE_CODES = 256;
+struct MailArgs {
+    MailRows m;
+    Publish pb;
+    uint8_t codes[MAIL_INLINE_CODES];
+};
+
 // The step kernel's body.  OBS (NCH = 1, A <= 8, k_obs_small's configurations): after the
 // write-back the wave builds the env's observations of the new state from the registers the
 // step leaves (robots on lanes < A, package j on lane j), as MAPPO/trainer.py:229-286 does
 // after every env.step -- one launch and no state reload instead of k_step + k_obs_small.
+// MAIL: after the write-back the wave writes its env's mailbox rows and counts itself toward
+// the call's completion word (MailArgs).
 // Sixteen-robot movement test: lane L compares robot L & 15 with robot 4 (L >> 4) + k;
 // the lanes where that partner has the lower index.
 __host__ __device__ constexpr uint64_t move_lt_lanes(int k) {
@@ -388,11 +418,12 @@ __host__ __device__ constexpr uint64_t move_lt_lanes(int k) {
     return m;
 }
 
-template <bool STALE, int NCH, bool FUSED, int AU, bool OBS>
+template <bool STALE, int NCH, bool FUSED, int AU, bool OBS, bool MAIL = false>
 __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, const uint64_t* __restrict__ pkg_pre,
                                           const uint16_t* __restrict__ pst_pre, const u32x4* __restrict__ es_pre,
                                           const uint64_t* __restrict__ trk_pre, const uint8_t* __restrict__ act_pre,
-                                          uint32_t ap, uint32_t nw, const StepArgs& args, const ObsArgs& oa) {
+                                          uint32_t ap, uint32_t nw, const StepArgs& args, const ObsArgs& oa,
+                                          const MailArgs* ma = nullptr) {
     static_assert(!OBS || (NCH == 1 && !FUSED && AU > 0 && AU <= 8), "fused observations: P <= 64, A <= 8");
     extern __shared__ __align__(16) unsigned char smem[];
     const DevParams& p = args.p;
@@ -1068,6 +1099,31 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
     if constexpr (OBS)   // full batch only (no env_ids): output row w = env e
         obs_small_emit<STALE>(p, w, mi, act ? rob_pack(cell, carry, vmask) : 0u, pk[0], ps[0], STALE ? td[0] : 0ull,
                               t_cur, oa.amap, oa.avec, oa.cmap, oa.cvec, smem + (size_t)wave * lds_stride);
+    if constexpr (MAIL) {   // row w of the call: k_mail_export's layout, from the registers
+        const MailRows& m = ma->m;
+        if (act) {
+            int32_t* o = m.robots + ((size_t)w * A + lane) * 3;
+            o[0] = cell_r(cell);
+            o[1] = cell_c(cell);
+            o[2] = carry;
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const int j = c * WAVE + lane;
+            if (j < P) {
+                int4* o = (int4*)(m.pkgs + ((size_t)w * P + j) * 8);
+                const uint64_t d = pk[c];
+                o[0] = int4{cell_r(pk_start(d)), cell_c(pk_start(d)), cell_r(pk_target(d)), cell_c(pk_target(d))};
+                o[1] = int4{pk_st(d), pk_dl(d), j + 1, (int)(ps[c] & PS_STATUS)};
+            }
+        }
+        if (lane == 0) {
+            m.t[w] = t_cur;
+            m.total[w] = tot_cur;
+            m.rterms[w] = (int32_t)rfl;
+        }
+        publish_tail(ma->pb);   // pb.expect = n: the waves of rows [0, n) count themselves
+    }
 }
 
 template <bool STALE, int NCH, bool FUSED, int AU>
@@ -1080,6 +1136,20 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict
                                                       uint32_t nw, StepArgs args) {
     step_body<STALE, NCH, FUSED, AU, false>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre, act_pre, ap, nw, args,
                                             ObsArgs{});
+}
+
+// mdl_mail_step: k_step + the mailbox rows + the completion word in one launch; the action
+// bytes come from the kernel arguments when they fit (ma.pb / codes: MailArgs)
+template <bool STALE, int NCH, int AU>
+__global__ __launch_bounds__(MDL_STEP_LB) void k_step_mail(const uint32_t* __restrict__ rob_pre,
+                                                           const uint64_t* __restrict__ pkg_pre,
+                                                           const uint16_t* __restrict__ pst_pre,
+                                                           const u32x4* __restrict__ es_pre,
+                                                           const uint64_t* __restrict__ trk_pre,
+                                                           const uint8_t* __restrict__ act_pre, uint32_t ap,
+                                                           uint32_t nw, StepArgs args, MailArgs ma, int inl) {
+    step_body<STALE, NCH, false, AU, false, true>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre,
+                                                  inl ? ma.codes : act_pre, ap, nw, args, ObsArgs{}, &ma);
 }
 
 // mdl_step_obs: k_step + k_obs_small in one launch (full batch, NCH = 1, A <= 8)
@@ -1271,23 +1341,6 @@ __device__ inline TrkView load_view(const int32_t* rec, ViewLdsPre& V, int& t, i
     }
     wave_sync();
     return TrkView{V.ids, V.flag, V.pk, ns};
-}
-
-// the completion tail of a Publish launch (every wave of the grid runs it); a one-wave launch
-// (ctr == nullptr) publishes straight after its release
-__device__ __forceinline__ void publish_tail(const Publish& pb) {
-    __atomic_thread_fence(__ATOMIC_RELEASE);   // this wave's stores, before it is counted
-    if (!pb.ctr) {
-        if (lane_id() == 0) __hip_atomic_store(pb.seq, pb.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-    }
-    if (lane_id() == 0) {
-        const unsigned waves = gridDim.x * (blockDim.x / WAVE);
-        if (atomicAdd(pb.ctr, 1u) - pb.base == waves - 1u) {   // the last wave of the grid
-            __atomic_thread_fence(__ATOMIC_ACQ_REL);
-            __hip_atomic_store(pb.seq, pb.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
 }
 
 // view record `rec`, agent index `a`, outputs row w
@@ -1733,6 +1786,52 @@ static void launch_step_s(const DevParams& p, const uint8_t* actions, int fmt, c
         case 8: launch_step_t<ST, 8, FUSED>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s); break;
         default: launch_step_t<ST, 16, FUSED>(p, actions, fmt, ids, n, auto_reset, r, sh, done, wpb, lds, K, s); break;
     }
+}
+
+template <bool ST, int NCH>
+static void launch_step_mail_t(const StepArgs& a, const uint8_t* actions, const MailArgs& ma, int inl, int wpb,
+                               size_t lds, hipStream_t s) {
+    const DevParams& p = a.p;
+    const dim3 grid(blocks_for(a.n, wpb)), block(64 * wpb);
+    const uint32_t ap = (uint32_t)p.A | ((uint32_t)p.P << 16);
+    const uint32_t nw = (uint32_t)a.n | ((uint32_t)wpb << 24) | (a.env_ids ? NW_IDS : 0u) | (p.env_map ? NW_MAP : 0u);
+#define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a, ma, inl
+    if (p.A <= 8) hipLaunchKernelGGL((k_step_mail<ST, NCH, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    else hipLaunchKernelGGL((k_step_mail<ST, NCH, 0>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+#undef MDL_STEP_ARGS
+}
+
+hipError_t launch_step_mail(const DevParams& p, const uint8_t* codes, const int* ids, int n, int auto_reset, double* r,
+                            float* sh, uint8_t* done, int wpb, size_t lds, const MailRows& m, unsigned* ctr,
+                            unsigned base, int32_t seq, hipStream_t s) {
+    StepArgs a;
+    a.p = p;
+    a.actions = codes;
+    a.env_ids = ids;
+    a.r_out = r;
+    a.sh_out = sh;
+    a.done_out = done;
+    a.fmt = 1;   // MDL_ACTION_CODES (decode_action)
+    a.n = n;
+    a.auto_reset = auto_reset;
+    a.wpb = wpb;
+    a.lds_stride = (int)lds;
+    a.K = 1;
+    MailArgs ma;
+    ma.m = m;
+    ma.pb = Publish{m.seq, ctr, base, seq, (unsigned)n};
+    const size_t nb = (size_t)n * p.A;
+    const int inl = nb <= (size_t)MAIL_INLINE_CODES;
+    if (inl) std::memcpy(ma.codes, codes, nb);
+    const bool st = p.stale != 0;
+    switch (nch_for(p.P)) {
+        case 1: st ? launch_step_mail_t<true, 1>(a, codes, ma, inl, wpb, lds, s) : launch_step_mail_t<false, 1>(a, codes, ma, inl, wpb, lds, s); break;
+        case 2: st ? launch_step_mail_t<true, 2>(a, codes, ma, inl, wpb, lds, s) : launch_step_mail_t<false, 2>(a, codes, ma, inl, wpb, lds, s); break;
+        case 4: st ? launch_step_mail_t<true, 4>(a, codes, ma, inl, wpb, lds, s) : launch_step_mail_t<false, 4>(a, codes, ma, inl, wpb, lds, s); break;
+        case 8: st ? launch_step_mail_t<true, 8>(a, codes, ma, inl, wpb, lds, s) : launch_step_mail_t<false, 8>(a, codes, ma, inl, wpb, lds, s); break;
+        default: st ? launch_step_mail_t<true, 16>(a, codes, ma, inl, wpb, lds, s) : launch_step_mail_t<false, 16>(a, codes, ma, inl, wpb, lds, s); break;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,

@@ -33,6 +33,7 @@ struct Publish {
     unsigned* ctr = nullptr;
     unsigned base = 0;
     int32_t value = 0;
+    unsigned expect = 0;   // > 0: the number of waves that count themselves (not the whole grid)
 };
 // A view record carried in the kernel arguments (mdl_host_view_*): two capacity classes, the larger
 // sized so the kernel's whole argument block stays well inside the 4 KiB kernarg limit.
@@ -67,6 +68,11 @@ struct MailRows {
     int32_t* rterms;   // [E] RT_* bits
 };
 hipError_t launch_publish(int32_t* seq, int32_t value, hipStream_t s);
+// mdl_mail_step in one launch: the step (action codes, rows [0, n) = envs ids[w] or w), its rows
+// into the mailbox, the completion word `seq` once all n waves have counted themselves in `ctr`
+hipError_t launch_step_mail(const DevParams& p, const uint8_t* codes, const int* ids, int n, int auto_reset, double* r,
+                            float* sh, uint8_t* done, int wpb, size_t lds, const MailRows& m, unsigned* ctr,
+                            unsigned base, int32_t seq, hipStream_t s);
 unsigned mail_export_waves(int n);   // waves of one k_mail_export launch over n envs
 hipError_t launch_mail_export(const DevParams& p, const int32_t* ids, int n, const MailRows& m, unsigned* ctr,
                               unsigned base, int32_t seq, hipStream_t s);

@@ -479,12 +479,147 @@ done:
     return ret;
 }
 
+/* ---- Environment.step on the mailbox in one C call ---- */
+typedef int (*mail_step_fn)(void* eng, int32_t n, int32_t use_ids, int32_t auto_reset, void* stream);
+typedef struct {
+    mail_step_fn step;
+    void* eng;
+    uint8_t* codes;
+    int32_t* ids;
+    const double* r_env;
+    const uint8_t* done;
+    const int32_t* robots;
+    const int32_t* pkgs;
+    const int32_t* t;
+    const double* total;
+    const int32_t* rterms;
+    int A, P;
+} MailCtx;
+
+static void mail_ctx_free(PyObject* cap) { PyMem_Free(PyCapsule_GetPointer(cap, "mdl.mailctx")); }
+
+/* mail_ctx(addr mdl_mail_step, eng, codes, ids, r_env, done, robots, pkgs, t, total, rterms, A, P) -> capsule */
+static PyObject* mail_ctx(PyObject* self, PyObject* args) {
+    unsigned long long f, eng, codes, ids, r_env, done, robots, pkgs, t, total, rterms;
+    int A, P;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "KKKKKKKKKKKii", &f, &eng, &codes, &ids, &r_env, &done, &robots, &pkgs, &t, &total,
+                          &rterms, &A, &P))
+        return NULL;
+    MailCtx* c = (MailCtx*)PyMem_Malloc(sizeof(MailCtx));
+    if (!c) return PyErr_NoMemory();
+    c->step = (mail_step_fn)(uintptr_t)f;
+    c->eng = (void*)(uintptr_t)eng;
+    c->codes = (uint8_t*)(uintptr_t)codes;
+    c->ids = (int32_t*)(uintptr_t)ids;
+    c->r_env = (const double*)(uintptr_t)r_env;
+    c->done = (const uint8_t*)(uintptr_t)done;
+    c->robots = (const int32_t*)(uintptr_t)robots;
+    c->pkgs = (const int32_t*)(uintptr_t)pkgs;
+    c->t = (const int32_t*)(uintptr_t)t;
+    c->total = (const double*)(uintptr_t)total;
+    c->rterms = (const int32_t*)(uintptr_t)rterms;
+    c->A = A;
+    c->P = P;
+    PyObject* cap = PyCapsule_New(c, "mdl.mailctx", mail_ctx_free);
+    if (!cap) PyMem_Free(c);
+    return cap;
+}
+
+/* get_state's dict from mailbox row 0 (env.py:127-147): 1-indexed robots, the packages whose
+ * start_time is t as (id, sr+1, sc+1, tr+1, tc+1, start_time, deadline) */
+static PyObject* state_dict(const MailCtx* c, PyObject* grid) {
+    const int A = c->A, P = c->P, t = c->t[0];
+    PyObject* rl = PyList_New(A);
+    if (!rl) return NULL;
+    for (int i = 0; i < A; i++) {
+        const int32_t* r = c->robots + 3 * i;
+        PyObject* tp = Py_BuildValue("(iii)", r[0] + 1, r[1] + 1, r[2]);
+        if (!tp) {
+            Py_DECREF(rl);
+            return NULL;
+        }
+        PyList_SET_ITEM(rl, i, tp);
+    }
+    PyObject* pl = PyList_New(0);
+    if (!pl) {
+        Py_DECREF(rl);
+        return NULL;
+    }
+    for (int j = 0; j < P; j++) {
+        const int32_t* q = c->pkgs + 8 * j;
+        if (q[4] != t) continue;
+        PyObject* tp = Py_BuildValue("(iiiiiii)", q[6], q[0] + 1, q[1] + 1, q[2] + 1, q[3] + 1, q[4], q[5]);
+        if (!tp || PyList_Append(pl, tp) < 0) {
+            Py_XDECREF(tp);
+            Py_DECREF(rl);
+            Py_DECREF(pl);
+            return NULL;
+        }
+        Py_DECREF(tp);
+    }
+    PyObject* d = Py_BuildValue("{s:i,s:O,s:N,s:N}", "time_step", t, "map", grid, "robots", rl, "packages", pl);
+    return d;
+}
+
+/* env_step(ctx, stream, actions, n_robots, idx (-1: the engine's only env), grid)
+ *   -> (state dict, r_env float, rterms int, done bool, t int, total float, robot rows bytes, package rows bytes)
+ * compat.Environment.step's engine part: the actions' codes (compat._code; a count other than
+ * n_robots raises env.py:182-183's ValueError) into the mailbox, mdl_mail_step, then the new
+ * state dict and the env's rows from the mailbox. */
+static PyObject* env_step(PyObject* self, PyObject* args) {
+    PyObject *cap, *actions, *grid;
+    unsigned long long stream;
+    int n_robots, idx;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "OKOiiO", &cap, &stream, &actions, &n_robots, &idx, &grid)) return NULL;
+    MailCtx* c = (MailCtx*)PyCapsule_GetPointer(cap, "mdl.mailctx");
+    if (!c) return NULL;
+    PyObject* acts = PySequence_Fast(actions, "actions must be a sequence");
+    if (!acts) return NULL;
+    const Py_ssize_t na = PySequence_Fast_GET_SIZE(acts);
+    if (na != n_robots || n_robots != c->A) {
+        Py_DECREF(acts);
+        PyErr_SetString(PyExc_ValueError, "The number of actions must match the number of robots.");
+        return NULL;
+    }
+    for (Py_ssize_t i = 0; i < na; i++) {
+        PyObject* pr = PySequence_Fast(PySequence_Fast_GET_ITEM(acts, i), "each action must be a (move, op) pair");
+        if (!pr) {
+            Py_DECREF(acts);
+            return NULL;
+        }
+        if (PySequence_Fast_GET_SIZE(pr) != 2) {
+            Py_DECREF(pr);
+            Py_DECREF(acts);
+            PyErr_SetString(PyExc_ValueError, "each action must be a (move, op) pair");
+            return NULL;
+        }
+        c->codes[i] = (uint8_t)(move_code(PySequence_Fast_GET_ITEM(pr, 0)) | (op_code(PySequence_Fast_GET_ITEM(pr, 1)) << 3));
+        Py_DECREF(pr);
+    }
+    Py_DECREF(acts);
+    if (idx >= 0) c->ids[0] = idx;
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = c->step(c->eng, 1, idx >= 0 ? 1 : 0, 0, (void*)(uintptr_t)stream);
+    Py_END_ALLOW_THREADS
+    if (rc) return lib_error("mdl_mail_step");
+    PyObject* st = state_dict(c, grid);
+    if (!st) return NULL;
+    return Py_BuildValue("(NdiOidy#y#)", st, c->r_env[0], (int)c->rterms[0], c->done[0] ? Py_True : Py_False,
+                         (int)c->t[0], c->total[0], (const char*)c->robots, (Py_ssize_t)(12 * c->A),
+                         (const char*)c->pkgs, (Py_ssize_t)(32 * c->P));
+}
+
 static PyMethodDef methods[] = {
     {"pack_view", pack_view, METH_VARARGS, "Pack a state view record into host memory; returns words written."},
     {"pack_robots", pack_robots, METH_VARARGS, "Pack a [t, A, robots] record into host memory."},
     {"bind", bind, METH_VARARGS, "Bind the engine's self-publishing helper entry points."},
     {"features", features, METH_VARARGS, "One helper featurizer call: pack, launch, wait, numpy outputs."},
     {"shaped", shaped, METH_VARARGS, "One compute_shaped_rewards call: pack, launch, wait, numpy.float32."},
+    {"mail_ctx", mail_ctx, METH_VARARGS, "The mailbox addresses of an engine, for env_step."},
+    {"env_step", env_step, METH_VARARGS, "Environment.step's engine part in one call."},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_mdl_pack", NULL, -1, methods, NULL, NULL, NULL, NULL};

@@ -126,6 +126,24 @@ def lib():
     return _lib
 
 
+_pack_bound = None
+
+
+def pack():
+    """The C extension of the per-call dict paths (_mdl_pack), bound once to libmdl.so's
+    entries it calls directly (helpers: mdl_host_view*_*; errors: mdl_last_error / MdlError)."""
+    global _pack_bound
+    if _pack_bound is None:
+        from . import _mdl_pack
+        L = lib()
+        addr = lambda f: C.cast(f, C.c_void_p).value  # noqa: E731
+        _mdl_pack.bind(addr(L.mdl_host_views_features), addr(L.mdl_host_views_shaped_reward),
+                       addr(L.mdl_host_view_features), addr(L.mdl_host_view_shaped_reward),
+                       addr(L.mdl_last_error), MdlError)
+        _pack_bound = _mdl_pack
+    return _pack_bound
+
+
 def check(rc: int, what: str = "") -> None:
     if rc != 0:
         msg = lib().mdl_last_error().decode(errors="replace")

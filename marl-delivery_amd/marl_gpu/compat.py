@@ -24,6 +24,8 @@ import operator
 import numpy as np
 
 from ._lib import MDL_RTERM_LATE, MDL_RTERM_MOVE, MDL_RTERM_ONTIME
+from ._lib import pack as _pack
+from ._lib import raw_stream as _raw_stream
 from .engine import STATUS_NAMES, BatchedEnv
 from .maps import grid_array, load_map, map_path
 
@@ -93,12 +95,27 @@ class _Slot:
         self._idx = idx
 
     def _set_rows(self, rob, pk, t, total):
-        self._rob = rob
-        self._pk = pk
+        """rob [A, 3] / pk [P, 8] int32 rows, as arrays or as their bytes (viewed on first use)."""
+        self._rob_v = rob
+        self._pk_v = pk
         self.t = int(t)
         self.total_reward = float(total)
         self._robots = None
         self._packages = None
+
+    @property
+    def _rob(self):
+        v = self._rob_v
+        if v.__class__ is bytes:
+            v = self._rob_v = np.frombuffer(v, np.int32).reshape(-1, 3)
+        return v
+
+    @property
+    def _pk(self):
+        v = self._pk_v
+        if v.__class__ is bytes:
+            v = self._pk_v = np.frombuffer(v, np.int32).reshape(-1, 8)
+        return v
 
     @property
     def robots(self):
@@ -165,6 +182,8 @@ class Environment(_Slot):
         self.engine = _engine
         self._mb = _engine.mailbox()
         self._single = _engine.E == 1
+        self._ctx = _engine.mail_ctx()
+        self._dev = _engine.device.index
         self.done = False
         self.state = None
 
@@ -188,17 +207,19 @@ class Environment(_Slot):
 
     # env.py:173-306
     def step(self, actions):
-        mb = self._mb
-        mb["codes"][0] = _encode(actions, self.n_robots)
-        self._call_one(self.engine.mail_step)
-        done = bool(mb["done"][0])
-        r = typed_reward(mb["r_env"][0], int(mb["rterms"][0]), self.move_cost, self.delivery_reward,
-                         self.delay_reward)
+        # one C call (_mdl_pack.env_step): the action codes into the mailbox, mdl_mail_step, the
+        # new state dict and this env's rows out of it
+        if actions.__class__ is not list and actions.__class__ is not tuple:
+            actions = list(actions)
+        st, r_env, rterms, done, t, total, rob, pk = _pack().env_step(
+            self._ctx, _raw_stream(self._dev), actions, self.n_robots, -1 if self._single else self._idx, self.grid)
+        self._set_rows(rob, pk, t, total)
+        r = typed_reward(r_env, rterms, self.move_cost, self.delivery_reward, self.delay_reward)
         infos = {}
         if done:
             infos["total_reward"] = self.total_reward
             infos["total_time_steps"] = self.t
-        return self._state_dict(), r, done, infos
+        return st, r, done, infos
 
     def check_terminate(self):
         if self.t == self.max_time_steps:

@@ -473,9 +473,21 @@ class BatchedEnv:
                       pkgs=arr(m.pkgs, C.c_int32, (E, P, 8)), t=arr(m.t, C.c_int32, (E,)),
                       total_reward=arr(m.total_reward, C.c_double, (E,)), rterms=arr(m.rterms, C.c_int32, (E,)))
             self._mb = mb
+            self._mbox = m
             L = lib()
             self._mail_fns = (L.mdl_mail_step, L.mdl_mail_reset, L.mdl_mail_export)
         return mb
+
+    def mail_ctx(self):
+        """The mailbox as the C extension's context (compat.Environment.step in one C call)."""
+        c = self.__dict__.get("_mail_ctx")
+        if c is None:
+            self.mailbox()
+            m = self._mbox
+            c = self._mail_ctx = _lib.pack().mail_ctx(
+                C.cast(lib().mdl_mail_step, C.c_void_p).value, self._h.value, m.codes, m.ids, m.r_env, m.done,
+                m.robots, m.pkgs, m.t, m.total_reward, m.rterms, self.A, self.P)
+        return c
 
     def mail_step(self, n: int, use_ids: bool, auto_reset: bool = False) -> None:
         """Step the mailbox's envs (``ids[:n]`` when use_ids, else all E, with ``codes[:n]``) and

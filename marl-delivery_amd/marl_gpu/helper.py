@@ -28,7 +28,7 @@ import ctypes as C
 import numpy as np
 
 from . import _mdl_pack
-from ._lib import check, lib
+from ._lib import check, lib, pack
 from .engine import MAPPO_SHAPING, QMIX_SHAPING, BatchedEnv
 from .compat import MOVE_CODES, OP_CODES, _code  # noqa: F401  (MOVE_CODES / OP_CODES re-exported)
 
@@ -60,21 +60,6 @@ def _engine_for(grid) -> BatchedEnv:
     return _arena_for(grid).eng
 
 
-_bound: list = [False]
-
-
-def _bind():
-    """Hand the C packer the engine's self-publishing helper entries (once)."""
-    if not _bound[0]:
-        from ._lib import MdlError
-        L = lib()
-        addr = lambda f: C.cast(f, C.c_void_p).value  # noqa: E731
-        _mdl_pack.bind(addr(L.mdl_host_views_features), addr(L.mdl_host_views_shaped_reward),
-                       addr(L.mdl_host_view_features), addr(L.mdl_host_view_shaped_reward),
-                       addr(L.mdl_last_error), MdlError)
-        _bound[0] = True
-
-
 class _Arena:
     """The engine's host-mapped arena (mdl_host_arena) as one numpy byte view; grows on demand
     (every call has finished with it on return: the helper calls are synchronous).  ``h`` /
@@ -82,7 +67,7 @@ class _Arena:
 
     def __init__(self, eng):
         import torch
-        _bind()
+        pack()
         self.eng = eng
         self.cap = 0
         self.addr = 0

@@ -31,6 +31,10 @@
 // is then streamed once as aligned float4s -- data float4s from the image, padding float4s as
 // zeros -- instead of a zero-filled slab overwritten by the tuples after a vmcnt(0) wait
 // (which wrote the tuple bytes twice).  Replaces the early fill when it applies.
+// Single-write streaming loops with clamped lane indices instead of per-iteration exec masks (1)
+#ifndef MDL_OBS_CLAMP
+#define MDL_OBS_CLAMP 1
+#endif
 #ifndef MDL_OBS_SINGLEWRITE
 #define MDL_OBS_SINGLEWRITE 1
 #endif
@@ -586,6 +590,37 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
             // at its last, so every gap float4 lies inside the slab.
             wave_sync();
             float4* a4 = reinterpret_cast<float4*>(avec);
+#if MDL_OBS_CLAMP
+            // The slab's two end float4s may hold a neighbouring env's floats: written per float
+            // by two lanes; every other float4 by uniform-trip loops in which lanes past a run's end
+            // repeat its last float4 (the same value: no exec-mask branches per iteration).
+            const int qh = g0 >> 2, qt = (g0 + S - 1) >> 2;   // the slab's first / last float4
+            const bool ph = (g0 & 3) != 0, pt = ((g0 + S) & 3) != 0;
+            if ((lane == 0 && ph) || (lane == 1 && pt)) {
+                const int q = lane == 0 ? qh : qt;
+                const int wi = lane == 0 ? 0 : nwin - 1;   // its window: the first / the last
+                const int4 wt = wtab[wi];
+                const float4 v = img4[wt.z + (q - wt.x)];
+                const int f0 = 4 * q - g0;
+                float* d = avec + 4 * (size_t)q;
+                if ((unsigned)f0 < (unsigned)S) d[0] = v.x;
+                if ((unsigned)(f0 + 1) < (unsigned)S) d[1] = v.y;
+                if ((unsigned)(f0 + 2) < (unsigned)S) d[2] = v.z;
+                if ((unsigned)(f0 + 3) < (unsigned)S) d[3] = v.w;
+            }
+            for (int wi = 0; wi < nwin; wi++) {   // uniform
+                const int4 wt = wtab[wi];
+                const int x0 = wt.x + ((wi == 0 && ph) ? 1 : 0);
+                const int y0 = wt.y - ((wi == nwin - 1 && pt) ? 1 : 0);
+                for (int q0 = x0; q0 < y0; q0 += WAVE) {   // uniform
+                    const int q = min(q0 + lane, y0 - 1);
+                    a4[q] = img4[wt.z + (q - wt.x)];
+                }
+                const int gend = wi + 1 < nwin ? wtab[wi + 1].x : wt.y;
+                for (int q0 = wt.y; q0 < gend; q0 += WAVE)   // uniform
+                    a4[min(q0 + lane, gend - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#else
             for (int wi = 0; wi < nwin; wi++) {   // uniform
                 const int4 wt = wtab[wi];
                 for (int q = wt.x + lane; q < wt.y; q += WAVE) {
@@ -604,6 +639,7 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
                 const int gend = wi + 1 < nwin ? wtab[wi + 1].x : wt.y;
                 for (int q = wt.y + lane; q < gend; q += WAVE) a4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
+#endif
         }
         // padding: other-robot slots [MOc, MO) and package slots [ns, MP) of every agent
         if (!sw && !av_early && (MO > MOc || MP > ns)) {

@@ -528,12 +528,14 @@ static PyObject* mail_ctx(PyObject* self, PyObject* args) {
 
 /* get_state's dict from mailbox row 0 (env.py:127-147): 1-indexed robots, the packages whose
  * start_time is t as (id, sr+1, sc+1, tr+1, tc+1, start_time, deadline) */
-static PyObject* state_dict(const MailCtx* c, PyObject* grid) {
-    const int A = c->A, P = c->P, t = c->t[0];
+static PyObject* state_dict(const MailCtx* c, int w, PyObject* grid) {
+    const int A = c->A, P = c->P, t = c->t[w];
+    const int32_t* robots = c->robots + (size_t)w * A * 3;
+    const int32_t* pkgs = c->pkgs + (size_t)w * P * 8;
     PyObject* rl = PyList_New(A);
     if (!rl) return NULL;
     for (int i = 0; i < A; i++) {
-        const int32_t* r = c->robots + 3 * i;
+        const int32_t* r = robots + 3 * i;
         PyObject* tp = Py_BuildValue("(iii)", r[0] + 1, r[1] + 1, r[2]);
         if (!tp) {
             Py_DECREF(rl);
@@ -547,7 +549,7 @@ static PyObject* state_dict(const MailCtx* c, PyObject* grid) {
         return NULL;
     }
     for (int j = 0; j < P; j++) {
-        const int32_t* q = c->pkgs + 8 * j;
+        const int32_t* q = pkgs + 8 * j;
         if (q[4] != t) continue;
         PyObject* tp = Py_BuildValue("(iiiiiii)", q[6], q[0] + 1, q[1] + 1, q[2] + 1, q[3] + 1, q[4], q[5]);
         if (!tp || PyList_Append(pl, tp) < 0) {
@@ -562,11 +564,70 @@ static PyObject* state_dict(const MailCtx* c, PyObject* grid) {
     return d;
 }
 
-/* env_step(ctx, stream, actions, n_robots, idx (-1: the engine's only env), grid)
- *   -> (state dict, r_env float, rterms int, done bool, t int, total float, robot rows bytes, package rows bytes)
- * compat.Environment.step's engine part: the actions' codes (compat._code; a count other than
- * n_robots raises env.py:182-183's ValueError) into the mailbox, mdl_mail_step, then the new
- * state dict and the env's rows from the mailbox. */
+/* the codes of one env's actions into row w of the mailbox (compat._code's mapping); a count other
+ * than n_robots raises env.py:182-183's ValueError */
+static int encode_into(uint8_t* row, int A, PyObject* actions, int n_robots) {
+    PyObject* acts = PySequence_Fast(actions, "actions must be a sequence");
+    if (!acts) return -1;
+    const Py_ssize_t na = PySequence_Fast_GET_SIZE(acts);
+    if (na != n_robots || n_robots != A) {
+        Py_DECREF(acts);
+        PyErr_SetString(PyExc_ValueError, "The number of actions must match the number of robots.");
+        return -1;
+    }
+    for (Py_ssize_t i = 0; i < na; i++) {
+        PyObject* pr = PySequence_Fast(PySequence_Fast_GET_ITEM(acts, i), "each action must be a (move, op) pair");
+        if (!pr) {
+            Py_DECREF(acts);
+            return -1;
+        }
+        if (PySequence_Fast_GET_SIZE(pr) != 2) {
+            Py_DECREF(pr);
+            Py_DECREF(acts);
+            PyErr_SetString(PyExc_ValueError, "each action must be a (move, op) pair");
+            return -1;
+        }
+        row[i] = (uint8_t)(move_code(PySequence_Fast_GET_ITEM(pr, 0)) | (op_code(PySequence_Fast_GET_ITEM(pr, 1)) << 3));
+        Py_DECREF(pr);
+    }
+    Py_DECREF(acts);
+    return 0;
+}
+
+static int encode_row(const MailCtx* c, int w, PyObject* actions, int n_robots) {
+    return encode_into(c->codes + (size_t)w * c->A, c->A, actions, n_robots);
+}
+
+/* encode(actions, n_robots) -> bytes: the mailbox's codes of one env's actions (host only; the
+ * tests hold it against compat.encode_actions) */
+static PyObject* encode(PyObject* self, PyObject* args) {
+    PyObject* actions;
+    int n_robots;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "Oi", &actions, &n_robots)) return NULL;
+    if (n_robots < 0 || n_robots > 64) {
+        PyErr_SetString(PyExc_ValueError, "0..64 robots");
+        return NULL;
+    }
+    uint8_t row[64];
+    if (encode_into(row, n_robots, actions, n_robots)) return NULL;
+    return PyBytes_FromStringAndSize((const char*)row, n_robots);
+}
+
+/* row w's results: (state dict, r_env float, rterms int, done bool, t int, total float, robot rows bytes,
+ * package rows bytes) */
+static PyObject* row_result(const MailCtx* c, int w, PyObject* grid) {
+    PyObject* st = state_dict(c, w, grid);
+    if (!st) return NULL;
+    return Py_BuildValue("(NdiOidy#y#)", st, c->r_env[w], (int)c->rterms[w], c->done[w] ? Py_True : Py_False,
+                         (int)c->t[w], c->total[w], (const char*)(c->robots + (size_t)w * c->A * 3),
+                         (Py_ssize_t)(12 * c->A), (const char*)(c->pkgs + (size_t)w * c->P * 8),
+                         (Py_ssize_t)(32 * c->P));
+}
+
+/* env_step(ctx, stream, actions, n_robots, idx (-1: the engine's only env), grid) -> row_result
+ * compat.Environment.step's engine part: the actions' codes into the mailbox, mdl_mail_step, then
+ * the new state dict and the env's rows from the mailbox. */
 static PyObject* env_step(PyObject* self, PyObject* args) {
     PyObject *cap, *actions, *grid;
     unsigned long long stream;
@@ -575,41 +636,72 @@ static PyObject* env_step(PyObject* self, PyObject* args) {
     if (!PyArg_ParseTuple(args, "OKOiiO", &cap, &stream, &actions, &n_robots, &idx, &grid)) return NULL;
     MailCtx* c = (MailCtx*)PyCapsule_GetPointer(cap, "mdl.mailctx");
     if (!c) return NULL;
-    PyObject* acts = PySequence_Fast(actions, "actions must be a sequence");
-    if (!acts) return NULL;
-    const Py_ssize_t na = PySequence_Fast_GET_SIZE(acts);
-    if (na != n_robots || n_robots != c->A) {
-        Py_DECREF(acts);
-        PyErr_SetString(PyExc_ValueError, "The number of actions must match the number of robots.");
-        return NULL;
-    }
-    for (Py_ssize_t i = 0; i < na; i++) {
-        PyObject* pr = PySequence_Fast(PySequence_Fast_GET_ITEM(acts, i), "each action must be a (move, op) pair");
-        if (!pr) {
-            Py_DECREF(acts);
-            return NULL;
-        }
-        if (PySequence_Fast_GET_SIZE(pr) != 2) {
-            Py_DECREF(pr);
-            Py_DECREF(acts);
-            PyErr_SetString(PyExc_ValueError, "each action must be a (move, op) pair");
-            return NULL;
-        }
-        c->codes[i] = (uint8_t)(move_code(PySequence_Fast_GET_ITEM(pr, 0)) | (op_code(PySequence_Fast_GET_ITEM(pr, 1)) << 3));
-        Py_DECREF(pr);
-    }
-    Py_DECREF(acts);
+    if (encode_row(c, 0, actions, n_robots)) return NULL;
     if (idx >= 0) c->ids[0] = idx;
     int rc;
     Py_BEGIN_ALLOW_THREADS
     rc = c->step(c->eng, 1, idx >= 0 ? 1 : 0, 0, (void*)(uintptr_t)stream);
     Py_END_ALLOW_THREADS
     if (rc) return lib_error("mdl_mail_step");
-    PyObject* st = state_dict(c, grid);
-    if (!st) return NULL;
-    return Py_BuildValue("(NdiOidy#y#)", st, c->r_env[0], (int)c->rterms[0], c->done[0] ? Py_True : Py_False,
-                         (int)c->t[0], c->total[0], (const char*)c->robots, (Py_ssize_t)(12 * c->A),
-                         (const char*)c->pkgs, (Py_ssize_t)(32 * c->P));
+    return row_result(c, 0, grid);
+}
+
+/* vec_step(ctx, stream, actions_per_row, n_robots, ids (None: rows are envs 0..n-1), grid)
+ *   -> [row_result, ...]: one mdl_mail_step over n distinct envs (compat.VectorizedEnv.step's rounds) */
+static PyObject* vec_step(PyObject* self, PyObject* args) {
+    PyObject *cap, *rows, *ids, *grid;
+    unsigned long long stream;
+    int n_robots;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "OKOiOO", &cap, &stream, &rows, &n_robots, &ids, &grid)) return NULL;
+    MailCtx* c = (MailCtx*)PyCapsule_GetPointer(cap, "mdl.mailctx");
+    if (!c) return NULL;
+    PyObject* rs = PySequence_Fast(rows, "actions must be a sequence");
+    if (!rs) return NULL;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(rs);
+    PyObject* out = NULL;
+    for (Py_ssize_t w = 0; w < n; w++)
+        if (encode_row(c, (int)w, PySequence_Fast_GET_ITEM(rs, w), n_robots)) goto done;
+    const int use_ids = ids != Py_None;
+    if (use_ids) {
+        PyObject* is = PySequence_Fast(ids, "ids must be a sequence");
+        if (!is) goto done;
+        if (PySequence_Fast_GET_SIZE(is) != n) {
+            Py_DECREF(is);
+            PyErr_SetString(PyExc_ValueError, "one id per action row");
+            goto done;
+        }
+        for (Py_ssize_t w = 0; w < n; w++) {
+            const long e = PyLong_AsLong(PySequence_Fast_GET_ITEM(is, w));
+            if (e == -1 && PyErr_Occurred()) {
+                Py_DECREF(is);
+                goto done;
+            }
+            c->ids[w] = (int32_t)e;
+        }
+        Py_DECREF(is);
+    }
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = c->step(c->eng, (int32_t)n, use_ids, 0, (void*)(uintptr_t)stream);
+    Py_END_ALLOW_THREADS
+    if (rc) {
+        lib_error("mdl_mail_step");
+        goto done;
+    }
+    out = PyList_New(n);
+    if (!out) goto done;
+    for (Py_ssize_t w = 0; w < n; w++) {
+        PyObject* r = row_result(c, (int)w, grid);
+        if (!r) {
+            Py_CLEAR(out);
+            goto done;
+        }
+        PyList_SET_ITEM(out, w, r);
+    }
+done:
+    Py_DECREF(rs);
+    return out;
 }
 
 static PyMethodDef methods[] = {
@@ -620,6 +712,8 @@ static PyMethodDef methods[] = {
     {"shaped", shaped, METH_VARARGS, "One compute_shaped_rewards call: pack, launch, wait, numpy.float32."},
     {"mail_ctx", mail_ctx, METH_VARARGS, "The mailbox addresses of an engine, for env_step."},
     {"env_step", env_step, METH_VARARGS, "Environment.step's engine part in one call."},
+    {"vec_step", vec_step, METH_VARARGS, "One VectorizedEnv.step round's engine part in one call."},
+    {"encode", encode, METH_VARARGS, "The action codes of one env's actions (host only)."},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_mdl_pack", NULL, -1, methods, NULL, NULL, NULL, NULL};

@@ -343,28 +343,23 @@ class VectorizedEnv:
             idx = self._index(list(indices)[:len(actions)])
             rounds = self._rounds(idx)
             full = False
-        eng, mb = self.engine, self._mb
+        if not idx:
+            raise ValueError("not enough values to unpack (expected 4, got 0)")   # zip(*[]) in the reference
         res = [None] * len(idx)
+        env0 = self.envs[0]
+        ctx, stream, grid = env0._ctx, _raw_stream(env0._dev), env0.grid
+        mc, dr, lr = env0.move_cost, env0.delivery_reward, env0.delay_reward
+        envs = self.envs
         for rnd in rounds:
             ids = [idx[p] for p in rnd]
-            n = len(ids)
-            codes = mb["codes"]
-            for k, (p, e) in enumerate(zip(rnd, ids)):
-                codes[k] = _encode(actions[p], self.envs[e].n_robots)
-            if not full:
-                mb["ids"][:n] = ids
-            eng.mail_step(n, not full)
-            r_h, d_h, rt_h = mb["r_env"][:n].tolist(), mb["done"][:n].tolist(), mb["rterms"][:n].tolist()
-            self._take_rows(ids)
-            for k, (p, e) in enumerate(zip(rnd, ids)):
-                env = self.envs[e]
-                info = {}
-                if d_h[k]:
-                    info = {"total_reward": env.total_reward, "total_time_steps": env.t}
-                res[p] = (env._state_dict(), typed_reward(r_h[k], rt_h[k], env.move_cost, env.delivery_reward,
-                                                          env.delay_reward), bool(d_h[k]), info)
-        if not res:
-            raise ValueError("not enough values to unpack (expected 4, got 0)")   # zip(*[]) in the reference
+            # one C call per round: codes in, mdl_mail_step, each row's state dict and rows out
+            rows = _pack().vec_step(ctx, stream, [actions[p] for p in rnd], env0.n_robots, None if full else ids,
+                                    grid)
+            for p, e, (st, r_env, rterms, done, t, total, rob, pk) in zip(rnd, ids, rows):
+                env = envs[e]
+                env._set_rows(rob, pk, t, total)
+                info = {"total_reward": env.total_reward, "total_time_steps": env.t} if done else {}
+                res[p] = (st, typed_reward(r_env, rterms, mc, dr, lr), done, info)
         states, rewards, dones, infos = (list(x) for x in zip(*res))
         return states, rewards, dones, infos
 

@@ -1,11 +1,3 @@
-mkdir -p gpurun_out/r03aa
-export TMPDIR=/tmp
-for MM in 100,100 4,5; do
-OBS_WHICH=all OBS_MO_MP=$MM timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_obs_small -d gpurun_out/r03aa/w_$MM -o run --output-format csv -- python3 scripts/exp/obs_parts.py > gpurun_out/r03aa/w_$MM.log 2>&1 || exit $?
-done
-python3 - <<'PY'
-import csv, glob, statistics
-for mm in ("100,100", "4,5"):
-    v = [float(r["Counter_Value"]) for f in glob.glob(f"gpurun_out/r03aa/w_{mm}/**/run_counter_collection.csv", recursive=True) for r in csv.DictReader(open(f)) if r["Counter_Name"] == "WRITE_SIZE"]
-    print(mm, "launches", len(v), "WRITE_SIZE median (KB)", statistics.median(v))
-PY
+mkdir -p gpurun_out/r03ab
+timeout -k 10 600 python -u -m pytest tests/test_gpu_compat.py tests/test_gpu_rollout.py tests/test_gpu_api.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r03ab/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/r03ab/pytest.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python scripts/exp/vec_cost.py > gpurun_out/r03ab/vec_cost.txt 2>&1; rc=$?; cat gpurun_out/r03ab/vec_cost.txt; [ $rc -ne 0 ] && exit $rc

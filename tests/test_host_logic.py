@@ -49,6 +49,26 @@ def test_encode_actions_codes_and_length_check():
         compat.encode_actions([("S", "0")], 2)
 
 
+def test_c_action_encoder_matches_compat():
+    """The C encoder the dict-API step uses (_mdl_pack.encode / env_step / vec_step) maps every
+    (move, op) the way compat._code does: the five move letters and '0'/'1'/'2', anything else
+    (other strings, ints, None, str subclasses) to the no-op codes 5 / 3."""
+    from marl_gpu import _mdl_pack
+
+    class S(str):
+        pass
+    vals = ["S", "L", "R", "U", "D", "0", "1", "2", "3", "", "SS", "s", 1, 0, None, 2.0, S("L"), S("1")]
+    rs = np.random.RandomState(3)
+    for _ in range(200):
+        n = int(rs.randint(0, 9))
+        acts = [(vals[rs.randint(len(vals))], vals[rs.randint(len(vals))]) for _ in range(n)]
+        assert _mdl_pack.encode(acts, n) == bytes(compat.encode_actions(acts, n).tolist()), acts
+    with pytest.raises(ValueError):
+        _mdl_pack.encode([("S", "0")], 2)
+    with pytest.raises(ValueError):
+        _mdl_pack.encode([("S", "0", "x")], 1)
+
+
 def test_align_and_c_packer_matches_numpy_layout():
     """The helper functions' dict packer (CPython extension _mdl_pack) writes the view record
     mdl_views_features reads: [t, A, n, map] + robots 0-indexed + tracker rows in dict order."""

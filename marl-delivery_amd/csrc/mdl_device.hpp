@@ -112,6 +112,21 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 // addressing and the map descriptor lookup are scalar
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
+// Workgroups are dealt round-robin to the 8 XCDs, each with its own L2: workgroup b of nb runs on
+// XCD b % 8.  xcd_block() renumbers them so that each XCD's workgroups take one contiguous range
+// of block slots: the envs of an XCD (and so every cache line of their rows, shared with
+// neighbours or not) are touched by that XCD alone, launch after launch, and each launch finds
+// the rows the previous one wrote in that XCD's L2 (scripts/exp/l2_retain.hip: the state round
+// trip 1344 -> 1020 cycles at 4096 envs).  A bijection on [0, nb).
+#ifndef MDL_XCD_REMAP
+#define MDL_XCD_REMAP 1
+#endif
+__device__ __forceinline__ int xcd_block() {
+    const int b = (int)blockIdx.x, nb = (int)gridDim.x;
+    if (!MDL_XCD_REMAP) return b;
+    return (b & 7) * (nb >> 3) + min(b & 7, nb & 7) + (b >> 3);
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p, const int* __restric
     extern __shared__ __align__(16) unsigned char smem[];
     const int wave = wave_id();
     const int lane = lane_id();
-    const int w = blockIdx.x * wpb + wave;
+    const int w = xcd_block() * wpb + wave;
     if (wave >= wpb || w >= n) return;
     const int e = env_ids ? env_ids[w] : w;
     if ((unsigned)e >= (unsigned)p.E) return;  // device-side ids: out of range -> skipped
@@ -446,7 +446,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
 
     const int wave = wave_id();
     const int lane = lane_id();
-    const int w = blockIdx.x * wpb_ + wave;
+    const int w = xcd_block() * wpb_ + wave;
     if (wave >= wpb_ || w >= n_) return;
     int e = w;
     if (nw & NW_IDS) {   // subset stepping: one more load; an id outside [0, E) is skipped
@@ -1194,7 +1194,7 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
     extern __shared__ __align__(16) unsigned char smem[];
     const int wave = wave_id();
     const int lane = lane_id();
-    const int w = blockIdx.x * wpb + wave;
+    const int w = xcd_block() * wpb + wave;
     if (wave >= wpb || w >= n) return;
     const int e = env_begin + w;
     const int A = p.A, P = p.P;

@@ -704,7 +704,7 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
     extern __shared__ __align__(16) unsigned char smem[];
     const int wave = wave_id();
     const int lane = lane_id();
-    const int w = blockIdx.x * wpb + wave;
+    const int w = xcd_block() * wpb + wave;
     if (wave >= wpb || w >= n) return;
     const int e = env_begin + w;
     const int A = p.A, P = p.P;

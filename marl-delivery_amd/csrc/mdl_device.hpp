@@ -121,10 +121,9 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 #ifndef MDL_XCD_REMAP
 #define MDL_XCD_REMAP 1
 #endif
+__device__ __forceinline__ int xcd_slot(int b, int nb) { return (b & 7) * (nb >> 3) + min(b & 7, nb & 7) + (b >> 3); }
 __device__ __forceinline__ int xcd_block() {
-    const int b = (int)blockIdx.x, nb = (int)gridDim.x;
-    if (!MDL_XCD_REMAP) return b;
-    return (b & 7) * (nb >> 3) + min(b & 7, nb & 7) + (b >> 3);
+    return MDL_XCD_REMAP ? xcd_slot((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
 }
 
 __device__ __forceinline__ void wave_sync() {

@@ -365,6 +365,13 @@ struct StepKarg {
     StepArgs args;
 };
 constexpr uint32_t NW_IDS = 1u << 29, NW_MAP = 1u << 30;
+// ap = A (7 bits) | P << 7 (11 bits) | the launch's block count << AP_NB_SHIFT (0 when it does not
+// fit: launch-order slots)
+constexpr int AP_NB_SHIFT = 18;
+inline uint32_t pack_ap(int A, int P, int nblocks) {
+    const uint32_t nb = (MDL_XCD_REMAP && nblocks < (1 << (32 - AP_NB_SHIFT))) ? (uint32_t)nblocks : 0u;
+    return (uint32_t)A | ((uint32_t)P << 7) | (nb << AP_NB_SHIFT);
+}
 
 // The fused step + observation launch's extra arguments (after StepArgs in its kernarg
 // segment, so the StepKarg prefix -- preloaded SGPRs, the late kernarg batch -- is the same).
@@ -434,7 +441,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
 #endif
     STAMP(0);
     // Preloaded (SGPR) arguments: everything the state loads need.
-    const int A = (int)(ap & 0xffffu), P = (int)(ap >> 16);
+    const int A = (int)(ap & 0x7fu), P = (int)((ap >> 7) & 0x7ffu);
     const int n_ = (int)(nw & 0xffffffu), wpb_ = (int)((nw >> 24) & 31u);
     GLOBAL const uint32_t* robp = (GLOBAL const uint32_t*)rob_pre;
     GLOBAL const uint64_t* pkgp = (GLOBAL const uint64_t*)pkg_pre;
@@ -446,7 +453,10 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
 
     const int wave = wave_id();
     const int lane = lane_id();
-    const int w = xcd_block() * wpb_ + wave;
+    // XCD-contiguous workgroup slots (xcd_block) from the block count packed in `ap` (a preloaded
+    // SGPR: gridDim.x would cost a dispatch-packet load ahead of every state load); 0 = launch order
+    const int nbp = (int)(ap >> AP_NB_SHIFT);
+    const int w = (nbp ? xcd_slot((int)blockIdx.x, nbp) : (int)blockIdx.x) * wpb_ + wave;
     if (wave >= wpb_ || w >= n_) return;
     int e = w;
     if (nw & NW_IDS) {   // subset stepping: one more load; an id outside [0, E) is skipped
@@ -1762,7 +1772,7 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
     a.lds_stride = (int)lds;
     a.K = K;
     const dim3 grid(blocks_for(n, wpb)), block(threads);
-    const uint32_t ap = (uint32_t)p.A | ((uint32_t)p.P << 16);
+    const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (ids ? NW_IDS : 0u) | (p.env_map ? NW_MAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a
     if (NCH <= 2 && p.A == 5)
@@ -1793,7 +1803,7 @@ static void launch_step_mail_t(const StepArgs& a, const uint8_t* actions, const 
                                size_t lds, hipStream_t s) {
     const DevParams& p = a.p;
     const dim3 grid(blocks_for(a.n, wpb)), block(64 * wpb);
-    const uint32_t ap = (uint32_t)p.A | ((uint32_t)p.P << 16);
+    const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
     const uint32_t nw = (uint32_t)a.n | ((uint32_t)wpb << 24) | (a.env_ids ? NW_IDS : 0u) | (p.env_map ? NW_MAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a, ma, inl
     if (p.A <= 8) hipLaunchKernelGGL((k_step_mail<ST, NCH, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
@@ -1862,7 +1872,7 @@ hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, 
     a.K = 1;
     const ObsArgs o{amap, avec, cmap, cvec};
     const dim3 grid(blocks_for(n, wpb)), block(64 * wpb);
-    const uint32_t ap = (uint32_t)p.A | ((uint32_t)p.P << 16);
+    const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a, o
     if (p.stale) {

@@ -90,6 +90,34 @@ __global__ __launch_bounds__(1024) void k_soa_pad(uint32_t* __restrict__ rob, co
     }
 }
 
+// per-env records (AoS) in the step's full shape: wpb envs per workgroup, XCD-contiguous slots,
+// the robot words, state words and env record written back
+__global__ __launch_bounds__(1024) void k_aos_full(unsigned char* __restrict__ rec, int n, int shift, int wpb,
+                                                   unsigned long long* __restrict__ cyc) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int w = ((b & 7) * (nb >> 3) + min(b & 7, nb & 7) + (b >> 3)) * wpb + wave;
+    const int lane = threadIdx.x & 63;
+    if (w >= n) return;
+    const int e = (w + shift) % n;
+    unsigned char* bb = rec + (size_t)e * REC;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    uint32_t r = lane < A ? ((uint32_t*)bb)[lane] : 0u;
+    uint64_t p = lane < P ? ((const uint64_t*)(bb + 64))[lane] : 0ull;
+    uint32_t s = lane < P ? ((const uint16_t*)(bb + 464))[lane] : 0u;
+    uint64_t t = lane < P ? ((const uint64_t*)(bb + 576))[lane] : 0ull;
+    const uint4 v = *(const uint4*)(bb + 976);
+    r += (uint32_t)p + s + (uint32_t)(t >> 7) + v.x;
+    asm volatile("" : "+v"(r));
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane < A) ((uint32_t*)bb)[lane] = r | 1u;
+    if (lane < P) ((uint16_t*)(bb + 464))[lane] = (uint16_t)(s + 1);
+    if (lane == 0) {
+        *(uint4*)(bb + 976) = uint4{v.x + 1, v.y, v.z, v.w};
+        cyc[w] = t1 - t0;
+    }
+}
+
 __global__ void k_flush(float4* p, size_t n4) {
     for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) p[i] = make_float4(1, 2, 3, 4);
 }
@@ -175,5 +203,23 @@ int main() {
                            pad == 1 ? "padded" : pad == 2 ? "packed_xcd" : "packed", wpb, E,
                            mode == 0 ? "same" : "flip", med[med.size() / 2]);
                 }
+    for (int wpb : {4, 16})
+        for (int E : {1024, 4096})
+            for (int mode = 0; mode < 2; mode++) {
+                std::vector<unsigned long long> med;
+                for (int it = 0; it < 40; it++) {
+                    const int shift = (mode == 1 && (it & 1)) ? E / 2 + 4 : 0;
+                    hipLaunchKernelGGL(k_aos_full, dim3(E / wpb), dim3(64 * wpb), 0, 0, rec, E, shift, wpb, cyc);
+                    CK(hipDeviceSynchronize());
+                    if (it < 10) continue;
+                    CK(hipMemcpy(h.data(), cyc, E * 8, hipMemcpyDeviceToHost));
+                    std::vector<unsigned long long> v(h.begin(), h.begin() + E);
+                    std::sort(v.begin(), v.end());
+                    med.push_back(v[E / 2]);
+                }
+                std::sort(med.begin(), med.end());
+                printf("{\"layout\": \"aos_full_xcd\", \"waves_per_block\": %d, \"envs\": %d, \"mode\": \"%s\", "
+                       "\"round_trip_cycles_median\": %llu}\n", wpb, E, mode == 0 ? "same" : "flip", med[med.size() / 2]);
+            }
     return 0;
 }

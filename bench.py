@@ -209,9 +209,19 @@ def main():
         graph.replay()
         torch.cuda.synchronize()
 
-    # warmup (eager steps, the same kernel)
-    for k in range(args.warmup):
-        one(k)
+    # warmup: W steps of the same kernel, launched the way the timed steps are (one replay of a
+    # W-step graph; eager launches without graphs)
+    if graph is not None and args.warmup > 0:
+        wg = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(wg, stream=s):
+                for k in range(args.warmup):
+                    one(k)
+        torch.cuda.synchronize()
+        wg.replay()
+    else:
+        for k in range(args.warmup):
+            one(k)
     torch.cuda.synchronize()
 
     def barrier():
@@ -231,9 +241,11 @@ def main():
 
     # ---- timed region: K steps replayed from graphs ----
     barrier()
-    t0 = time.perf_counter()
+    # the opening HIP event is enqueued on the idle stream before the clock starts: it marks the
+    # GPU-side start of the region (kernel_us below) and is not part of the K steps' work
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
+    t0 = time.perf_counter()
     if graph is not None:
         for _ in range(n_graph):
             graph.replay()

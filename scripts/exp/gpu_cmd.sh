@@ -1,10 +1,3 @@
-mkdir -p gpurun_out/r03am
-timeout -k 10 600 python -u -m pytest tests/test_gpu_bench_dist.py tests/test_gpu_api.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/r03am/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/r03am/pytest.log; [ $rc -ne 0 ] && exit $rc
-for rep in 1 2 3; do
-  timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r03am/driver_$rep.json 2>/dev/null || exit $?
-  python3 -c "
-import json; d=json.loads(open('gpurun_out/r03am/driver_$rep.json').read().strip().splitlines()[-1]); print('driver', $rep, 'value %.3e' % d['value'], 'us/step %.2f' % (d['ms_per_step']*1e3), 'event %.2f' % (d['gpu_event_ms_per_step']*1e3), 'frac %.4f' % d['roofline']['frac'], 'cpu', d['cpu_baseline']['value'] if d['cpu_baseline'] else None)"
-done
-timeout -k 10 300 python bench.py --cpu-seconds 0 --steps 2000 --warmup 100 > gpurun_out/r03am/long.json 2>/dev/null || exit $?
-python3 -c "
-import json; d=json.loads(open('gpurun_out/r03am/long.json').read().strip().splitlines()[-1]); print('long value %.3e' % d['value'], 'us/step %.3f' % (d['ms_per_step']*1e3))"
+mkdir -p gpurun_out/r03an
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_gpu_rollout.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r03an/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/r03an/pytest.log; [ $rc -ne 0 ] && exit $rc
+VARIANTS="head nu2 main nu8" REPS=3 CONFIG=5 STEPS=400 BENCH_EXTRA="--total-envs 16384" bash scripts/exp/ab_bench.sh || exit $?

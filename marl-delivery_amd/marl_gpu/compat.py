@@ -211,6 +211,8 @@ class Environment(_Slot):
         # new state dict and this env's rows out of it
         if actions.__class__ is not list and actions.__class__ is not tuple:
             actions = list(actions)
+        if self.engine._h is None:
+            raise RuntimeError("the environment's engine was closed")
         st, r_env, rterms, done, t, total, rob, pk = _pack().env_step(
             self._ctx, _raw_stream(self._dev), actions, self.n_robots, -1 if self._single else self._idx, self.grid)
         self._set_rows(rob, pk, t, total)
@@ -345,6 +347,8 @@ class VectorizedEnv:
             full = False
         if not idx:
             raise ValueError("not enough values to unpack (expected 4, got 0)")   # zip(*[]) in the reference
+        if self.engine._h is None:
+            raise RuntimeError("the environments' engine was closed")
         res = [None] * len(idx)
         env0 = self.envs[0]
         ctx, stream, grid = env0._ctx, _raw_stream(env0._dev), env0.grid

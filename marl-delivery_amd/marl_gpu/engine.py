@@ -137,6 +137,9 @@ class BatchedEnv:
     # ------------------------------------------------------------------ core
     def close(self):
         if getattr(self, "_h", None):
+            # the mailbox context (compat's C step path) holds raw engine addresses: drop it first
+            self.__dict__.pop("_mail_ctx", None)
+            self.__dict__.pop("_mb", None)
             lib().mdl_destroy(self._h)
             self._h = None
 

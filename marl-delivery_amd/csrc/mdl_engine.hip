@@ -83,15 +83,17 @@ struct DeviceGuard {
     }
 };
 
-// Waves per workgroup of the step kernel for a launch over n envs.  A batch that fills the
-// chip in one round of at least 4 waves per CU runs as ONE workgroup per CU (4..16 waves:
-// fewer workgroups to dispatch; config 2's 4096 envs = 16 waves on each of 256 CUs,
-// 4.47 -> 4.40 us per step); larger batches keep 4-wave workgroups, which finish and free
-// their CU slot independently (16-wave workgroups measured 6-12 % slower at 8192 and 16384
-// envs).  Capped by the LDS budget (the reset scratch per wave).
+// Waves per workgroup of the step kernel for a launch over n envs: 4 (capped by the LDS budget,
+// the reset scratch per wave).  Round 2 ran a chip-filling batch as ONE workgroup per CU (config
+// 2's 4096 envs = 16 waves on each of 256 CUs: 4.47 -> 4.40 us per step then); with the
+// XCD-contiguous slots (xcd_block) 4-wave workgroups are faster again: config 2 4.34-4.35 ->
+// 4.22-4.25 us same box, 2- and 1-wave workgroups 4.24-4.27 / 4.38-4.40, config 5 unchanged
+// (profiles/r03/step_wpb_ab.txt).
 int step_wpb(int n, int n_cu, size_t lds_per_wave, int P) {
+    (void)n;
+    (void)n_cu;
+    (void)P;
     int w = 4;
-    if (P <= 128 && n_cu > 0 && n >= 4 * n_cu && n <= 16 * n_cu) w = (n + n_cu - 1) / n_cu;   // 1024-thread bound: NCH <= 2
     if (lds_per_wave > 0) {
         const int cap = (int)(LDS_BUDGET / lds_per_wave);
         if (w > cap) w = cap;

@@ -327,9 +327,8 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 // one launch with the state held in registers between them; actions [K][n][A],
 // outputs [K][n].  FUSED=false is the API's one step per launch (K = 1).
 #ifndef MDL_STEP_WPB
-// up to 16 waves per workgroup (the engine's step_wpb) for the one- and two-chunk package
-// tables (<= 61 VGPRs); the larger ones keep 256-thread workgroups and their registers
-#define MDL_STEP_LB (NCH <= 2 ? 1024 : 256)
+// at most 4 waves per workgroup (the engine's step_wpb)
+#define MDL_STEP_LB 256
 #else
 #define MDL_STEP_LB (64 * MDL_STEP_WPB)
 #endif
@@ -1164,7 +1163,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step_mail(const uint32_t* __res
 
 // mdl_step_obs: k_step + k_obs_small in one launch (full batch, NCH = 1, A <= 8)
 template <bool STALE, int AU>
-__global__ __launch_bounds__(1024) void k_step_obs(const uint32_t* __restrict__ rob_pre,
+__global__ __launch_bounds__(256) void k_step_obs(const uint32_t* __restrict__ rob_pre,
                                                   const uint64_t* __restrict__ pkg_pre,
                                                   const uint16_t* __restrict__ pst_pre,
                                                   const u32x4* __restrict__ es_pre,

@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches only (PMC profiling passes)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend under torchrun (gloo: rehearse N ranks on fewer GPUs)")
+    ap.add_argument("--host-wait", default="auto", choices=("auto", "spin", "yield", "blocking"),
+                    help="how the host waits for the GPU in synchronize (hipSetDeviceFlags schedule mode)")
     ap.add_argument("--graph-only", action="store_true",
                     help="skip the eager and isolated-launch legs (rocprof kernel-trace pass: the trace then holds "
                          "only the warmup and the timed graph replay, so its average is the timed region's)")
@@ -132,6 +134,20 @@ def cpu_threads():
     return max(1, min(16, n))
 
 
+HIP_SCHEDULE = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}   # hipDeviceSchedule* flags
+
+
+def set_host_wait(mode):
+    """hipSetDeviceFlags(schedule mode) on the current device: how a synchronize waits for
+    the GPU (spin: the host thread polls the completion signal instead of sleeping on it).
+    Returns the hipError_t (None for the HIP default, which is left untouched)."""
+    if mode == "auto":
+        return None
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    return int(hip.hipSetDeviceFlags(ctypes.c_uint(HIP_SCHEDULE[mode])))
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -152,6 +168,7 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    host_wait_rc = set_host_wait(args.host_wait)
 
     import marl_gpu
     from marl_gpu.maps import grid_array, load_map, map_path
@@ -340,6 +357,8 @@ def main():
             "steps": K,
             "warmup": args.warmup,
             "graph_upload_replay_steps": 0 if graph is None else G,
+            "graph_steps": 0 if graph is None else G,
+            "host_wait": args.host_wait if host_wait_rc in (None, 0) else f"{args.host_wait} (hipError {host_wait_rc})",
             "ms_per_step": wall / K * 1e3,
             "higher_is_better": True,
             "scaling": "strong" if args.total_envs > 0 else "weak",

@@ -332,6 +332,20 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 #else
 #define MDL_STEP_LB (64 * MDL_STEP_WPB)
 #endif
+// Waves per SIMD the step kernels (k_step, k_step_obs) are compiled for.  Left to itself the
+// compiler spends 106 SGPRs, which allows 7 waves per SIMD; amdgpu_waves_per_eu(8) keeps the SGPRs
+// within the 8-wave budget at the same instruction count (+1 VALU).  Same-box A/B
+// (profiles/r03/wpe8_ab.txt): config 5 (131072 envs) 113.7 -> 99.5 us per step, its 16384-env slice
+// 16.6 -> 15.3, config 4 34.3 -> 31.5; config 2 (4 waves per SIMD) and k_step_obs unchanged;
+// the general builder k_obs 1.3 % slower with it, so it keeps the compiler's choice.  0: no attribute.
+#ifndef MDL_STEP_WPE
+#define MDL_STEP_WPE 8
+#endif
+// Only the one- and two-chunk (P <= 128) per-launch forms: the fused bench kernel and the wider
+// package chunkings need more registers than the 8-wave budget and would spill (1 = no constraint).
+template <int NCH, bool FUSED>
+constexpr int step_wpe() { return (MDL_STEP_WPE > 0 && NCH <= 2 && !FUSED) ? MDL_STEP_WPE : 1; }
+#define MDL_STEP_ATTR(NCH, FUSED) __attribute__((amdgpu_waves_per_eu(step_wpe<NCH, FUSED>())))
 // AU > 0: A <= AU robots (AU = 8, or AU = A exactly for the configs' A = 5 and 16) -- the
 // per-robot scans are unrolled over AU lanes (independent
 // readlanes, no loop-carried branch), the latency-critical form at the configs' A = 5.
@@ -1136,7 +1150,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
 }
 
 template <bool STALE, int NCH, bool FUSED, int AU>
-__global__ __launch_bounds__(MDL_STEP_LB) void k_step(const uint32_t* __restrict__ rob_pre,
+__global__ __launch_bounds__(MDL_STEP_LB) MDL_STEP_ATTR(NCH, FUSED) void k_step(const uint32_t* __restrict__ rob_pre,
                                                       const uint64_t* __restrict__ pkg_pre,
                                                       const uint16_t* __restrict__ pst_pre,
                                                       const u32x4* __restrict__ es_pre,
@@ -1163,7 +1177,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step_mail(const uint32_t* __res
 
 // mdl_step_obs: k_step + k_obs_small in one launch (full batch, NCH = 1, A <= 8)
 template <bool STALE, int AU>
-__global__ __launch_bounds__(256) void k_step_obs(const uint32_t* __restrict__ rob_pre,
+__global__ __launch_bounds__(256) MDL_STEP_ATTR(1, false) void k_step_obs(const uint32_t* __restrict__ rob_pre,
                                                   const uint64_t* __restrict__ pkg_pre,
                                                   const uint16_t* __restrict__ pst_pre,
                                                   const u32x4* __restrict__ es_pre,

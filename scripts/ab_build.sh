@@ -1,13 +1,13 @@
 #!/bin/bash
 # Build an A/B variant of libmdl.so (profiling only): the CURRENT csrc/mdl_kernels.hip (plus
-# extra -D flags in $DEFS) linked with the production objects of the other files, into
+# extra flags in $DEFS, after the Makefile's kernel flags) linked with the production objects of the other files, into
 # marl-delivery_amd/build/ab/libmdl_<name>.so.  Usage: scripts/ab_build.sh <name>
 set -e
 N=${1:?name}
 cd "$(dirname "$0")/../marl-delivery_amd"
 mkdir -p build/ab
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt"
-/opt/rocm/bin/hipcc $F -mllvm -amdgpu-kernarg-preload-count=14 ${DEFS:-} -I../include -Icsrc -c csrc/mdl_kernels.hip \
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-kernarg-preload-count=14 -mllvm -amdgpu-sched-strategy=max-ilp ${DEFS:-} -I../include -Icsrc -c csrc/mdl_kernels.hip \
     -o build/ab/k_$N.o
 /opt/rocm/bin/hipcc $F -shared -o build/ab/libmdl_$N.so build/ab/k_$N.o build/mdl_engine.o build/mdl_rollout.o \
     build/mdl_greedy.o

@@ -25,6 +25,14 @@ def median_counter(d, counter, kern):
     return (vals[len(vals) // 2], len(vals)) if vals else (None, 0)
 
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rel(path):
+    """Repo-relative form of a path, so the record reads the same on any box."""
+    return os.path.relpath(os.path.abspath(path), REPO)
+
+
 def main():
     out, cal_path = sys.argv[1], sys.argv[2]
     cal = json.load(open(cal_path))
@@ -48,11 +56,11 @@ def main():
             "fetch_size_bytes_median": fetch, "fetch_dispatches": nf,
             "read_bytes_corrected": read_bytes,
             "write_bytes": write, "write_dispatches": nw,
-            "source": f"{d} (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, eager launches, medians; "
+            "source": f"{rel(d)} (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, eager launches, medians; "
                       f"KB x1024); FETCH_SIZE / {ratio:.4f}: the counted-over-read ratio measured for the step's own "
-                      f"access shapes by scripts/exp/fetch_cal.hip ({cal_path}, row 'step_shape', hot)",
+                      f"access shapes by scripts/exp/fetch_cal.hip ({rel(cal_path)}, row 'step_shape', hot)",
         })
-    json.dump({"calibration": cal_path, "fetch_ratio": ratio, "records": recs}, open(out, "w"), indent=1)
+    json.dump({"calibration": rel(cal_path), "fetch_ratio": ratio, "records": recs}, open(out, "w"), indent=1)
     print(json.dumps(recs, indent=1))
 
 

@@ -111,27 +111,53 @@ def cpu_baseline(args, grid, seeds0, budget_s, n_threads, E, map_name):
         ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS, n_threads=n_threads)
         t_all += time.perf_counter() - t0
         steps += 1
-    cpu_model = platform.processor()
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    host = host_cpu_info()
     how = "single thread" if n_threads == 1 else f"{n_threads} OpenMP threads"
     return {"value": E * A * steps / t_all, "unit": "agent-steps/s", "cores": n_threads, "kind": "port",
             "sample": f"{E} envs ({map_name}) x {steps} steps ({E * A * steps} agent-steps, {t_all:.1f} s) of the "
-                      f"same workload, oracle/mdl_oracle.c, {how}, host {cpu_model}"}
+                      f"same workload, oracle/mdl_oracle.c, {how}, host {host['lscpu_model_name']}",
+            "host": host,
+            "threads_note": f"threads = min(affinity {host['affinity_cpus']}, cap {host['thread_cap']}): the cap is "
+                            f"a one-GPU box's CPU share; nproc {host['nproc']} counts the whole machine"}
+
+
+CPU_THREAD_CAP = 16   # a one-GPU box's CPU share (the pool's limit: nproc shows the whole machine)
+
+
+def host_cpu_info():
+    """What the CPU leg ran on: ``nproc`` (the whole machine on a GPU box), this process's
+    affinity count, the ``lscpu`` model name, and the thread cap applied."""
+    def run(cmd):
+        try:
+            return subprocess.run(cmd, capture_output=True, text=True, timeout=10).stdout
+        except (OSError, subprocess.SubprocessError):
+            return ""
+    nproc = run(["nproc", "--all"]).strip()
+    model = ""
+    for line in run(["lscpu"]).splitlines():
+        if line.startswith("Model name:"):
+            model = line.split(":", 1)[1].strip()
+            break
+    if not model:
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            model = platform.processor()
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return {"nproc": int(nproc) if nproc.isdigit() else os.cpu_count(), "affinity_cpus": aff,
+            "lscpu_model_name": model, "thread_cap": CPU_THREAD_CAP,
+            "threads_used": max(1, min(CPU_THREAD_CAP, aff))}
 
 
 def cpu_threads():
-    """This process's CPU share: the affinity mask, capped at 16 (a one-GPU box's share)."""
-    try:
-        n = len(os.sched_getaffinity(0))
-    except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    """This process's CPU share: the affinity mask, capped at CPU_THREAD_CAP (reported beside it)."""
+    return host_cpu_info()["threads_used"]
 
 
 HIP_SCHEDULE = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}   # hipDeviceSchedule* flags

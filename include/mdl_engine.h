@@ -141,7 +141,9 @@ int mdl_views_idq_reward(MdlEngine* eng, const int32_t* prev_views, const int64_
  * distance field for every cell of every map (maps of <= 4096 cells).
  * mdl_greedy_actions = one get_actions(state) per listed env (call once per step, before
  * mdl_step), written as MDL_ACTION_CODES bytes [n][A].  Bug-compatible with the reference
- * agent (duplicated t=0 package entries, id-1 list indexing). */
+ * agent (duplicated t=0 package entries, id-1 list indexing).  After mdl_load_state of a
+ * checkpoint without greedy records, only a call without an id list (env_ids == NULL: every env)
+ * makes mdl_greedy_actions usable again. */
 int mdl_greedy_init(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* stream);
 int mdl_greedy_actions(MdlEngine* eng, const int32_t* env_ids, int32_t n, uint8_t* actions, void* stream);
 

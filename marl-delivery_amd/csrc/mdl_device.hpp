@@ -16,6 +16,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Profiling-only switches change what the kernels compute (skipped sections, missing stores,
+// no LDS request) or add diagnostic stores: they are accepted only in a build that says it is
+// one (-DMDL_PROFILING_BUILD), never in the product library.
+#if !defined(MDL_PROFILING_BUILD) && \
+    (defined(MDL_EXP_NOWAIT) || defined(MDL_EXP_NOTUPLES) || defined(MDL_EXP_NOLDS) || defined(MDL_ABLATE) || \
+     defined(MDL_STAMPS))
+#error "MDL_EXP_NOWAIT / MDL_EXP_NOTUPLES / MDL_EXP_NOLDS / MDL_ABLATE / MDL_STAMPS need -DMDL_PROFILING_BUILD"
+#endif
+
 namespace mdl {
 
 constexpr int WAVE = 64;

@@ -565,6 +565,8 @@ int mdl_mailbox(MdlEngine* eng, MdlMailbox* out) {
         }
         // fine-grained (coherent) and mapped: the kernels read the inputs and write the rows in place,
         // the host reads them as soon as the completion word changes
+        // the completion counter first: a mailbox exists only with everything it needs
+        if (!eng->mail_ctr && eng->alloc(&eng->mail_ctr, 1)) return -1;
         HIPCHK(hipHostMalloc(&eng->mail, tot, hipHostMallocCoherent | hipHostMallocMapped));
         memset(eng->mail, 0, tot);
         char* b = (char*)eng->mail;
@@ -580,7 +582,6 @@ int mdl_mailbox(MdlEngine* eng, MdlMailbox* out) {
         m.t = (int32_t*)(b + off[8]);
         m.total_reward = (double*)(b + off[9]);
         m.rterms = (int32_t*)(b + off[10]);
-        if (eng->alloc(&eng->mail_ctr, 1)) return -1;
         eng->mail_seen.assign(E, 0);
     }
     *out = eng->mbox;
@@ -744,8 +745,9 @@ int mdl_greedy_init(MdlEngine* eng, const int32_t* env_ids, int32_t n, void* str
     if (greedy_alloc(eng, s)) return -1;
     if (n == 0) return 0;
     HIPCHK(mdl::launch_greedy_init(eng->p, eng->glay, eng->gstate, env_ids, n, s));
-    // every env re-initialised: no id list, or a list of E ids (ids are unique by contract)
-    if (!env_ids || n == eng->p.E) eng->greedy_stale = false;
+    // every env re-initialised only without an id list: a device id list is not read back, and one
+    // of length E may repeat ids or hold ids the kernel skips
+    if (!env_ids) eng->greedy_stale = false;
     return 0;
 }
 
@@ -754,7 +756,7 @@ int mdl_greedy_actions(MdlEngine* eng, const int32_t* env_ids, int32_t n, uint8_
     if (!eng->gstate) return fail("mdl_greedy_actions: call mdl_greedy_init first");
     if (eng->greedy_stale)
         return fail("mdl_greedy_actions: the greedy agents' state predates mdl_load_state of a checkpoint without "
-                    "it; call mdl_greedy_init for every env (no id list, or all E ids)");
+                    "it; call mdl_greedy_init without an id list");
     if (!env_ids) n = eng->p.E;
     if (n < 0 || n > eng->p.E) return fail("mdl_greedy_actions: n=%d out of range", n);
     if (n == 0) return 0;

@@ -14,6 +14,10 @@
  * whose addresses bind() receives once), wait, and return the numpy outputs -- no ctypes call and
  * no Python-level buffer handling per call.
  *
+ * The GIL stays held across each call: the mailbox, the arena and their host-side counters are
+ * shared per engine, so two threads stepping envs of one engine (or calling helpers on one map)
+ * must not interleave -- the GIL serialises them (the calls are microseconds long).
+ *
  * Host plumbing only (no GPU code, no reference semantics beyond the record layout).  The tracker
  * dict is read in insertion order (PyDict_Next), the order the reference iterates
  * persistent_packages.values() in (MAPPO/trainer.py:95-130); 'status' == 'in_transit' -> 2, else 1.
@@ -330,20 +334,16 @@ static PyObject* features(PyObject* self, PyObject* args) {
     if (inl) {
         int32_t rec[MDL_VIEW_INLINE_WORDS];
         if (do_pack_view(rec, vw, t, robots, tracker, H, W, 0, -1) < 0) return NULL;
-        Py_BEGIN_ALLOW_THREADS
         rc = f_features1((void*)(uintptr_t)eng, rec, (int32_t)vw, (int32_t)idx, (int32_t)T, (int32_t)MO, (int32_t)MP,
                          (int32_t)MR, (int32_t)MPs, outp[0], outp[1], outp[2], outp[3], (void*)(uintptr_t)stream);
-        Py_END_ALLOW_THREADS
         if (rc) return lib_error("mdl_host_view_features");
     } else {
         if (do_pack_view((int32_t*)b, vw, t, robots, tracker, H, W, 0, -1) < 0) return NULL;
         *(int64_t*)(b + o_off) = 0;
         *(int32_t*)(b + o_idx) = (int32_t)idx;
-        Py_BEGIN_ALLOW_THREADS
         rc = f_features((void*)(uintptr_t)eng, (const int32_t*)b, (const int64_t*)(b + o_off), 1, (int32_t)ns,
                         (const int32_t*)(b + o_idx), (int32_t)T, (int32_t)MO, (int32_t)MP, (int32_t)MR, (int32_t)MPs,
                         outp[0], outp[1], outp[2], outp[3], (void*)(uintptr_t)stream);
-        Py_END_ALLOW_THREADS
         if (rc) return lib_error("mdl_host_views_features");
     }
     PyObject* tup = PyTuple_New(nout);
@@ -453,20 +453,16 @@ static PyObject* shaped(PyObject* self, PyObject* args) {
     int rc;
     const double* cp = consts ? (const double*)(uintptr_t)consts : NULL;
     if (inl) {
-        Py_BEGIN_ALLOW_THREADS
         rc = f_shaped1((void*)(uintptr_t)eng, rec, (int32_t)vw, rec + vw, (int32_t)cw, (const uint8_t*)(rec + vw + cw),
                        (int32_t)Na, g, cp, (float*)(b + o_out), (void*)(uintptr_t)stream);
-        Py_END_ALLOW_THREADS
     } else {
         *(int64_t*)(b + o_off) = 0;
         *(int64_t*)(b + o_off + 8) = 0;
         *(double*)(b + o_off + 16) = g;
-        Py_BEGIN_ALLOW_THREADS
         rc = f_shaped((void*)(uintptr_t)eng, (const int32_t*)b, (const int64_t*)(b + o_off), (int32_t)ns,
                       (const int32_t*)(b + o_c), (const int64_t*)(b + o_off), (const uint8_t*)(b + o_a),
                       (const int64_t*)(b + o_off), (const double*)(b + o_off + 16), 1, cp, (float*)(b + o_out),
                       (void*)(uintptr_t)stream);
-        Py_END_ALLOW_THREADS
     }
     if (rc) {
         lib_error(inl ? "mdl_host_view_shaped_reward" : "mdl_host_views_shaped_reward");
@@ -639,9 +635,7 @@ static PyObject* env_step(PyObject* self, PyObject* args) {
     if (encode_row(c, 0, actions, n_robots)) return NULL;
     if (idx >= 0) c->ids[0] = idx;
     int rc;
-    Py_BEGIN_ALLOW_THREADS
     rc = c->step(c->eng, 1, idx >= 0 ? 1 : 0, 0, (void*)(uintptr_t)stream);
-    Py_END_ALLOW_THREADS
     if (rc) return lib_error("mdl_mail_step");
     return row_result(c, 0, grid);
 }
@@ -682,9 +676,7 @@ static PyObject* vec_step(PyObject* self, PyObject* args) {
         Py_DECREF(is);
     }
     int rc;
-    Py_BEGIN_ALLOW_THREADS
     rc = c->step(c->eng, (int32_t)n, use_ids, 0, (void*)(uintptr_t)stream);
-    Py_END_ALLOW_THREADS
     if (rc) {
         lib_error("mdl_mail_step");
         goto done;

@@ -16,7 +16,13 @@ import os
 import torch  # noqa: F401  (must precede loading libmdl.so, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MDL_LIB_PATH") or os.path.join(HERE, "libmdl.so")  # override: profiling builds only
+# MDL_LIB_PATH loads another build of the library (same-box A/B of profiling builds): honoured only
+# with MDL_PROFILING=1, so no product run can pick up a profiling build by accident
+_PROFILING = os.environ.get("MDL_PROFILING") == "1"
+if os.environ.get("MDL_LIB_PATH") and not _PROFILING:
+    raise ImportError("marl_gpu: MDL_LIB_PATH is set without MDL_PROFILING=1; it selects a profiling build of "
+                      "libmdl.so and is refused otherwise")
+LIB_PATH = (os.environ.get("MDL_LIB_PATH") if _PROFILING else None) or os.path.join(HERE, "libmdl.so")
 
 MDL_TRACKER_FRESH = 0
 MDL_TRACKER_MAPPO_STALE = 1
@@ -117,7 +123,7 @@ def lib():
                               "(or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            if "MDL_LIB_PATH" in os.environ and not hasattr(L, name):
+            if _PROFILING and LIB_PATH != os.path.join(HERE, "libmdl.so") and not hasattr(L, name):
                 continue   # an older profiling build (same-box A/B): entry points it lacks stay unbound
             fn = getattr(L, name)
             fn.restype = res

@@ -14,11 +14,16 @@ when they have arrived -- no device staging buffers, copies or stream syncs.
 the int ``0`` and adds the move costs / delivery rewards (env.py:256,288,291),
 so the result is the int 0 when no term fired, a float once a float constant
 was added (also when the terms cancel to 0.0), and an int when only int
-constants were added.  ``render_pygame`` is a no-op (headless); ``render``
-prints text as the reference's ``render`` does.
+constants were added.  ``total_reward`` (and ``infos['total_reward']``) likewise: the
+int 0 after a reset (env.py:34,89), an int while every step's reward was an int, a float once
+one was a float (``self.total_reward += r``, env.py:297,303).  ``render_pygame`` is a no-op
+(headless); ``render`` prints text as the reference's ``render`` does.
+
+Not thread-safe per engine: the envs of one ``VectorizedEnv`` share its mailbox.
 """
 from __future__ import annotations
 
+import numbers
 import operator
 
 import numpy as np
@@ -54,13 +59,20 @@ def encode_actions(actions, n_robots):
     return np.array(_encode(actions, n_robots), np.uint8)
 
 
+def _is_int(c):
+    return isinstance(c, numbers.Integral)
+
+
 def typed_reward(r, rterms, move_cost, delivery_reward, delay_reward):
-    """The value env.step returns, with the reference's type (env.py:181,256,288,291)."""
+    """The value env.step returns, with the reference's type (env.py:181,256,288,291): the int 0
+    when no term fired, an int when every fired term's constant is integral, a float otherwise
+    (any non-integral constant: Python floats, numpy floating scalars, ...; the value is the
+    engine's fp64 sum)."""
     if not rterms:
         return 0
-    if (rterms & MDL_RTERM_MOVE and isinstance(move_cost, float)) or \
-            (rterms & MDL_RTERM_ONTIME and isinstance(delivery_reward, float)) or \
-            (rterms & MDL_RTERM_LATE and isinstance(delay_reward, float)):
+    if (rterms & MDL_RTERM_MOVE and not _is_int(move_cost)) or \
+            (rterms & MDL_RTERM_ONTIME and not _is_int(delivery_reward)) or \
+            (rterms & MDL_RTERM_LATE and not _is_int(delay_reward)):
         return float(r)
     return int(r)
 
@@ -90,16 +102,19 @@ class _Slot:
     call that touched it.  The ``robots`` / ``packages`` object lists are built on first access
     after a refresh (the state dict is built from the row arrays directly)."""
 
+    _tot_float = False   # a float reward was added since the last reset (env.py:89,297)
+
     def __init__(self, owner, idx):
         self._owner = owner
         self._idx = idx
 
     def _set_rows(self, rob, pk, t, total):
-        """rob [A, 3] / pk [P, 8] int32 rows, as arrays or as their bytes (viewed on first use)."""
+        """rob [A, 3] / pk [P, 8] int32 rows, as arrays or as their bytes (viewed on first use).
+        ``total`` is the engine's fp64 running total; its Python type follows ``_tot_float``."""
         self._rob_v = rob
         self._pk_v = pk
         self.t = int(t)
-        self.total_reward = float(total)
+        self.total_reward = float(total) if self._tot_float else int(total)
         self._robots = None
         self._packages = None
 
@@ -187,9 +202,16 @@ class Environment(_Slot):
         self.done = False
         self.state = None
 
+    def _live_mailbox(self):
+        """The engine's mailbox views, refused once the engine is closed (its host allocation
+        is freed by mdl_destroy, so the views must not be written)."""
+        if self.engine._h is None:
+            raise RuntimeError("the environment's engine was closed")
+        return self._mb
+
     def _call_one(self, fn):
         """One mailbox call on this env alone; refreshes this env's rows."""
-        mb = self._mb
+        mb = self._live_mailbox()
         if not self._single:
             mb["ids"][0] = self._idx
         fn(1, not self._single)
@@ -197,6 +219,7 @@ class Environment(_Slot):
 
     # env.py:81-125
     def reset(self):
+        self._tot_float = False                 # env.py:89: total_reward = 0
         self._call_one(self.engine.mail_reset)
         self.done = False
         self.state = None
@@ -215,8 +238,10 @@ class Environment(_Slot):
             raise RuntimeError("the environment's engine was closed")
         st, r_env, rterms, done, t, total, rob, pk = _pack().env_step(
             self._ctx, _raw_stream(self._dev), actions, self.n_robots, -1 if self._single else self._idx, self.grid)
-        self._set_rows(rob, pk, t, total)
         r = typed_reward(r_env, rterms, self.move_cost, self.delivery_reward, self.delay_reward)
+        if r.__class__ is float:
+            self._tot_float = True              # env.py:297: total_reward += r
+        self._set_rows(rob, pk, t, total)
         infos = {}
         if done:
             infos["total_reward"] = self.total_reward
@@ -252,7 +277,8 @@ class Environment(_Slot):
         for row in grid_copy:
             print("\t".join(str(cell) for cell in row))
 
-    def render_pygame(self, cell_size=40):  # headless engine
+    def render_pygame(self, cell_size=40, window_pos=(100, 100), **kwargs):
+        """Headless engine: accepts MAPPO/marl_delivery/env.py:362's signature and draws nothing."""
         return None
 
 
@@ -283,11 +309,18 @@ class VectorizedEnv:
         self.engine.mail_export(num_envs, False)   # every env's constructor layout (env.py:41)
         self._take_rows(list(range(num_envs)))
 
+    def _live_mailbox(self):
+        if self.engine._h is None:
+            raise RuntimeError("the environments' engine was closed")
+        return self._mb
+
     def _take_rows(self, ids):
-        """Refresh the envs of the last mailbox call (row k = env ids[k])."""
-        rob, pk, t, tot = _rows(self._mb, len(ids))
+        """Refresh the envs of the last mailbox call, a reset (row k = env ids[k])."""
+        rob, pk, t, tot = _rows(self._live_mailbox(), len(ids))
         for k, e in enumerate(ids):
-            self.envs[e]._set_rows(rob[k], pk[k], t[k], tot[k])
+            env = self.envs[e]
+            env._tot_float = False              # env.py:89: total_reward = 0
+            env._set_rows(rob[k], pk[k], t[k], tot[k])
 
     def _index(self, indices):
         """``self.envs[i]`` semantics of the reference's loops: negatives count from the
@@ -317,6 +350,7 @@ class VectorizedEnv:
 
     def reset(self, indices=None):
         eng = self.engine
+        mb = self._live_mailbox()
         if indices is None:
             eng.mail_reset(self.num_envs, False)
             self._take_rows(list(range(self.num_envs)))
@@ -325,7 +359,7 @@ class VectorizedEnv:
         out = [None] * len(idx)
         for rnd in self._rounds(idx):
             ids = [idx[p] for p in rnd]
-            self._mb["ids"][:len(ids)] = ids
+            mb["ids"][:len(ids)] = ids
             eng.mail_reset(len(ids), True)
             self._take_rows(ids)
             for p in rnd:
@@ -361,9 +395,12 @@ class VectorizedEnv:
                                     grid)
             for p, e, (st, r_env, rterms, done, t, total, rob, pk) in zip(rnd, ids, rows):
                 env = envs[e]
+                r = typed_reward(r_env, rterms, mc, dr, lr)
+                if r.__class__ is float:
+                    env._tot_float = True
                 env._set_rows(rob, pk, t, total)
                 info = {"total_reward": env.total_reward, "total_time_steps": env.t} if done else {}
-                res[p] = (st, typed_reward(r_env, rterms, mc, dr, lr), done, info)
+                res[p] = (st, r, done, info)
         states, rewards, dones, infos = (list(x) for x in zip(*res))
         return states, rewards, dones, infos
 

@@ -7,7 +7,7 @@ N=${1:?name}
 cd "$(dirname "$0")/../marl-delivery_amd"
 mkdir -p build/ab
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt"
-/opt/rocm/bin/hipcc $F -mllvm -amdgpu-kernarg-preload-count=14 -mllvm -amdgpu-sched-strategy=max-ilp ${DEFS:-} -I../include -Icsrc -c csrc/mdl_kernels.hip \
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-kernarg-preload-count=14 -mllvm -amdgpu-sched-strategy=max-ilp -DMDL_PROFILING_BUILD ${DEFS:-} -I../include -Icsrc -c csrc/mdl_kernels.hip \
     -o build/ab/k_$N.o
 /opt/rocm/bin/hipcc $F -shared -o build/ab/libmdl_$N.so build/ab/k_$N.o build/mdl_engine.o build/mdl_rollout.o \
     build/mdl_greedy.o

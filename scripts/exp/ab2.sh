@@ -5,17 +5,17 @@
 set -u
 mkdir -p gpurun_out/ab2
 if [ "${TESTS:-1}" = "1" ]; then
-  MDL_LIB_PATH=marl-delivery_amd/build/ablate/libmdl_B.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
+  MDL_PROFILING=1 MDL_LIB_PATH=marl-delivery_amd/build/ablate/libmdl_B.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
       -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/ab2/pytest_B.log 2>&1
   rc=$?; tail -2 gpurun_out/ab2/pytest_B.log; [ $rc -ne 0 ] && exit $rc
 fi
 for rep in 1 2 3; do
   for V in A B; do
     L=marl-delivery_amd/build/ablate/libmdl_$V.so
-    MDL_LIB_PATH=$L timeout -k 10 200 python bench.py --steps 2000 --warmup 100 --cpu-seconds 0 \
+    MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 200 python bench.py --steps 2000 --warmup 100 --cpu-seconds 0 \
         > gpurun_out/ab2/c2_${V}_$rep.json 2>/dev/null || exit 1
-    MDL_LIB_PATH=$L timeout -k 10 200 python scripts/bench_configs.py --config 4 > gpurun_out/ab2/c4_${V}_$rep.json 2>/dev/null || exit 1
-    MDL_LIB_PATH=$L timeout -k 10 200 python scripts/bench_configs.py --config 5 > gpurun_out/ab2/c5_${V}_$rep.json 2>/dev/null || exit 1
+    MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 200 python scripts/bench_configs.py --config 4 > gpurun_out/ab2/c4_${V}_$rep.json 2>/dev/null || exit 1
+    MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 200 python scripts/bench_configs.py --config 5 > gpurun_out/ab2/c5_${V}_$rep.json 2>/dev/null || exit 1
     python3 - <<EOF
 import json
 l = lambda f: json.loads(open(f).read().strip().splitlines()[-1])

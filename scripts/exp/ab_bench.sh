@@ -9,7 +9,7 @@ mkdir -p $O
 for rep in $(seq 1 ${REPS:-3}); do
   for V in ${VARIANTS:-main}; do
     if [ "$V" = main ]; then L=$R/marl-delivery_amd/marl_gpu/libmdl.so; else L=$R/marl-delivery_amd/build/ab/libmdl_$V.so; fi
-    MDL_LIB_PATH=$L timeout -k 10 120 python3 $R/bench.py --config ${CONFIG:-2} ${BENCH_EXTRA:-} --cpu-seconds 0 --fused-k 0 --graph-only \
+    MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 120 python3 $R/bench.py --config ${CONFIG:-2} ${BENCH_EXTRA:-} --cpu-seconds 0 --fused-k 0 --graph-only \
         --steps ${STEPS:-2000} --warmup 100 > $O/${V}_$rep.json 2> $O/${V}_$rep.err || exit $?
     python3 -c "
 import json

@@ -8,7 +8,7 @@ mkdir -p $O
 for rep in $(seq 1 ${REPS:-2}); do
   for V in ${VARIANTS:-main}; do
     if [ "$V" = main ]; then L=$R/marl-delivery_amd/marl_gpu/libmdl.so; else L=$R/marl-delivery_amd/build/ab/libmdl_$V.so; fi
-    MDL_LIB_PATH=$L timeout -k 10 200 python3 $R/scripts/bench_configs.py --config ${CONFIG:-3b} --steps 100 --warmup 10 \
+    MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 200 python3 $R/scripts/bench_configs.py --config ${CONFIG:-3b} --steps 100 --warmup 10 \
         > $O/${V}_$rep.json 2> $O/${V}_$rep.err || exit $?
     python3 -c "
 import json

@@ -12,8 +12,8 @@ for V in ${VARIANTS:-0 1 2 4 8 16 32 64}; do
   O=$R/gpurun_out/${OUT:-c2ab}/$V
   mkdir -p $O
   L=$R/marl-delivery_amd/build/ablate/libmdl_$V.so
-  MDL_LIB_PATH=$L timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex "k_step" -d $O/sq -o run --output-format csv -- python3 $R/bench.py ${BENCH_ARGS:-} --no-graph --cpu-seconds 0 --fused-k 0 --graph-only --steps 300 --warmup 20 > $O/sq.log 2>&1 || exit $?
-  MDL_LIB_PATH=$L timeout -k 10 120 python3 $R/bench.py ${BENCH_ARGS:-} --cpu-seconds 0 --fused-k 0 --graph-only --steps 2000 --warmup 100 > $O/bench.json 2> $O/bench.err || exit $?
+  MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex "k_step" -d $O/sq -o run --output-format csv -- python3 $R/bench.py ${BENCH_ARGS:-} --no-graph --cpu-seconds 0 --fused-k 0 --graph-only --steps 300 --warmup 20 > $O/sq.log 2>&1 || exit $?
+  MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 120 python3 $R/bench.py ${BENCH_ARGS:-} --cpu-seconds 0 --fused-k 0 --graph-only --steps 2000 --warmup 100 > $O/bench.json 2> $O/bench.err || exit $?
   python3 - <<PY
 import csv, glob, collections, json
 agg = collections.defaultdict(list)

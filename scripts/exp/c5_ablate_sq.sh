@@ -8,7 +8,7 @@ R=$(pwd)
 for V in ${VARIANTS:-0 1 2 4 8 32 64}; do
   O=$R/gpurun_out/c5ab/$V
   mkdir -p $O
-  MDL_LIB_PATH=$R/marl-delivery_amd/build/ablate/libmdl_$V.so timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES --kernel-include-regex "k_step" -d $O/sq -o run --output-format csv -- python3 $R/scripts/bench_configs.py --config 5 --steps 100 --warmup 5 > $O/sq.log 2>&1 || exit $?
+  MDL_PROFILING=1 MDL_LIB_PATH=$R/marl-delivery_amd/build/ablate/libmdl_$V.so timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES --kernel-include-regex "k_step" -d $O/sq -o run --output-format csv -- python3 $R/scripts/bench_configs.py --config 5 --steps 100 --warmup 5 > $O/sq.log 2>&1 || exit $?
   python3 - <<PY
 import csv, glob, collections
 agg = collections.defaultdict(list)

@@ -6,7 +6,7 @@ VARIANTS="prev main" REPS=2 CONFIG=4 STEPS=400 bash scripts/exp/ab_bench.sh || e
 CONFIG=3 VARIANTS="prev main" REPS=2 bash scripts/exp/ab_obs.sh || exit $?
 for rep in 1 2; do for V in prev main; do
   if [ "$V" = main ]; then L=$PWD/marl-delivery_amd/marl_gpu/libmdl.so; else L=$PWD/marl-delivery_amd/build/ab/libmdl_$V.so; fi
-  MDL_LIB_PATH=$L timeout -k 10 120 python bench.py --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/r03as/${V}_$rep.json 2>/dev/null || exit $?
+  MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 120 python bench.py --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/r03as/${V}_$rep.json 2>/dev/null || exit $?
   python3 -c "
 import json; d=json.loads(open('gpurun_out/r03as/${V}_$rep.json').read().strip().splitlines()[-1]); print('driver $V', $rep, 'value %.3e' % d['value'], 'us/step %.2f' % (d['ms_per_step']*1e3))"
 done; done

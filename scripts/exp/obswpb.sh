@@ -7,7 +7,7 @@ for rep in 1 2; do
   for V in A B4 B8 B16; do
     case $V in A) L=A; W=;; B4) L=B; W=4;; B8) L=B; W=8;; B16) L=B; W=16;; esac
     for C in 3 3b; do
-      o=$(MDL_OBS_WPB=$W MDL_LIB_PATH=marl-delivery_amd/build/ablate/libmdl_$L.so timeout -k 10 200 python scripts/bench_configs.py --config $C 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('obs %.2f fused %.2f' % (d['obs_us'], d['step_obs_fused_us']))") || exit 1
+      o=$(MDL_OBS_WPB=$W MDL_PROFILING=1 MDL_LIB_PATH=marl-delivery_amd/build/ablate/libmdl_$L.so timeout -k 10 200 python scripts/bench_configs.py --config $C 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('obs %.2f fused %.2f' % (d['obs_us'], d['step_obs_fused_us']))") || exit 1
       echo "$V $rep config $C $o"
     done
   done

@@ -1,6 +1,6 @@
 """Per-section cycle costs of k_step from the MDL_STAMPS diagnostic build (profiling only).
 
-Run with MDL_LIB_PATH=marl-delivery_amd/build/stamps/libmdl.so."""
+Run with MDL_PROFILING=1 MDL_LIB_PATH=marl-delivery_amd/build/stamps/libmdl.so."""
 import ctypes as C
 import json
 import os

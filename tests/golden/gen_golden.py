@@ -607,21 +607,28 @@ def gen_reward_types(ref, quick):
         rs = np.random.RandomState(aseed)
         acts = np.zeros((n, A, 2), np.uint8)   # (move code, op code) per robot
         r_l, rint_l, done_l = [], [], []
+        tot_l, tint_l, itint_l = [], [], []   # env.total_reward and infos['total_reward'] (env.py:34,89,297,303)
         for k in range(n):
             moves = rs.randint(0, 5, size=A)
             ops = rs.choice(3, size=A, p=[0.2, 0.4, 0.4])
             actions = [("SLRUD"[mv], str(op)) for mv, op in zip(moves, ops)]
             acts[k] = [enc_action(*a) for a in actions]
-            _, r, done, _ = env.step(actions)
+            _, r, done, infos = env.step(actions)
             r_l.append(float(r))
             rint_l.append(isinstance(r, int))
             done_l.append(bool(done))
+            tot_l.append(float(env.total_reward))
+            tint_l.append(isinstance(env.total_reward, int))
+            itint_l.append(isinstance(infos["total_reward"], int) if done else False)
             if done:
                 env.reset()
         arrays[f"acts_{ci}"] = acts
         arrays[f"r_{ci}"] = np.array(r_l, np.float64)
         arrays[f"rint_{ci}"] = np.array(rint_l, np.bool_)
         arrays[f"done_{ci}"] = np.array(done_l, np.bool_)
+        arrays[f"tot_{ci}"] = np.array(tot_l, np.float64)
+        arrays[f"tint_{ci}"] = np.array(tint_l, np.bool_)
+        arrays[f"itint_{ci}"] = np.array(itint_l, np.bool_)
         zf = int(np.sum((~arrays[f"rint_{ci}"]) & (arrays[f"r_{ci}"] == 0.0)))
         ni = int(np.sum(arrays[f"rint_{ci}"] & (arrays[f"r_{ci}"] != 0.0)))
         meta.append(dict(map=m, A=A, P=P, T=T, seed=seed, n=n, consts=[mc, dr, lr],

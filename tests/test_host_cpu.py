@@ -201,3 +201,36 @@ def test_step_kernels_fit_eight_waves_without_scratch(tmp_path):
     spill = sorted(n for n, r in res.items() if r.get("private_segment_fixed_size", 0) > 0
                    and re.search(r"k_step|k_obs|k_reset|k_seed", n))
     assert not spill, spill
+
+
+_PROFILING_SWITCHES = ["MDL_EXP_NOWAIT", "MDL_EXP_NOTUPLES", "MDL_EXP_NOLDS", "MDL_ABLATE=1", "MDL_STAMPS"]
+
+
+@pytest.mark.parametrize("switch", _PROFILING_SWITCHES)
+def test_profiling_switches_need_a_profiling_build(switch):
+    """A switch that changes what the kernels compute is an #error unless the build says it is a
+    profiling build; with -DMDL_PROFILING_BUILD it preprocesses."""
+    pkg = os.path.join(REPO, "marl-delivery_amd")
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "--cuda-device-only", "-std=c++17", "-E",
+           "-I", os.path.join(REPO, "include"), "-I", os.path.join(pkg, "csrc"),
+           os.path.join(pkg, "csrc", "mdl_kernels.hip"), "-o", os.devnull]
+    bad = subprocess.run(cmd + ["-D" + switch], capture_output=True, text=True)
+    assert bad.returncode != 0 and "MDL_PROFILING_BUILD" in bad.stderr, bad.stderr[-500:]
+    ok = subprocess.run(cmd + ["-D" + switch, "-DMDL_PROFILING_BUILD"], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr[-500:]
+
+
+def test_product_library_has_no_profiling_code():
+    """The shipped libmdl.so carries no diagnostic stamp buffer (MDL_STAMPS builds define g_stamps)."""
+    from marl_gpu import _lib
+    assert b"g_stamps" not in open(_lib.LIB_PATH, "rb").read()
+
+
+def test_lib_path_override_needs_profiling_flag():
+    """MDL_LIB_PATH selects a profiling build; without MDL_PROFILING=1 the import refuses it
+    instead of loading another library."""
+    env = dict(os.environ, MDL_LIB_PATH="/nonexistent/libmdl.so")
+    env.pop("MDL_PROFILING", None)
+    env["PYTHONPATH"] = os.path.join(REPO, "marl-delivery_amd")
+    r = subprocess.run([sys.executable, "-c", "import marl_gpu._lib"], env=env, capture_output=True, text=True)
+    assert r.returncode != 0 and "MDL_PROFILING=1" in r.stderr, r.stderr[-500:]

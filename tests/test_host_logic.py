@@ -116,3 +116,19 @@ def test_shards_cover_every_env_once():
         assert sorted(seen) == list(range(total))
     ids, seeds = D.shard(4096, 3, 42)
     assert ids[0] == 3 * 4096 and len(ids) == 4096 and seeds[0] == 42 + 3 * 4096
+
+
+def test_typed_reward_follows_constant_types():
+    """env.py:181 ``r = 0`` plus the fired terms' constants: the int 0 when none fired, an int
+    when every fired constant is integral (numpy integers included), a float otherwise --
+    numpy floating constants too (np.float32 must not truncate through int())."""
+    M, ON, LATE = compat.MDL_RTERM_MOVE, compat.MDL_RTERM_ONTIME, compat.MDL_RTERM_LATE
+    tr = compat.typed_reward
+    assert tr(0.0, 0, -0.01, 10.0, 1.0) == 0 and type(tr(0.0, 0, -0.01, 10.0, 1.0)) is int
+    r = tr(-0.03, M, np.float32(-0.01), 10, 1)
+    assert type(r) is float and r == -0.03
+    assert type(tr(-3.0, M, np.int32(-1), 10, 1)) is int
+    assert type(tr(10.0, ON, -0.01, 10, 1)) is int          # only the int constant fired
+    assert type(tr(9.99, ON | M, -0.01, 10, 1)) is float
+    assert type(tr(1.0, LATE, 0, 10, np.float64(1.0))) is float
+    assert type(tr(1.0, LATE, 0, 10, True)) is int

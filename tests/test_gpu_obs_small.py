@@ -102,3 +102,46 @@ def test_small_builder_config3_vs_oracle():
                 np.testing.assert_array_equal(cv[e], gv)
                 np.testing.assert_array_equal(cm[e], gm)
     env.close()
+
+
+@pytest.mark.parametrize("case", [("map.txt", 4, 20, 30, 6, 8, 3, 10), ("map1.txt", 5, 50, 60, 100, 100, 100, 100),
+                                  ("map4.txt", 3, 30, 40, 2, 5, 4, 7)],
+                         ids=["7x7", "config3b", "19x20"])
+def test_flat_emission_any_alignment_and_range(case):
+    """The flat emission pass (csrc/mdl_obs_expand.hpp) writes every float of each tensor exactly
+    once, wherever the tensor starts inside a 16-B line (lead 0..3 floats), with float4s that
+    straddle envs / planes / agents (HW % 4 != 0, vector lengths % 4 != 0), and for an env
+    sub-range: bit-identical to the aligned full build, the sentinels around each tensor intact."""
+    mg = _mg()
+    m, A, P, T, MO, MP, MR, MPs = case
+    g = grid(m)
+    H, W = g.shape
+    E = 37
+    env = mg.BatchedEnv(g, E, A, P, T, seed=3, tracker="mappo", max_other_robots=MO, max_packages_obs=MP,
+                        max_robots_state=MR, max_packages_state=MPs)
+    env.reset()
+    gen = np.random.RandomState(8)
+    for _ in range(T // 2 + 3):
+        env.step(torch.from_numpy(gen.randint(0, 15, size=(E, A)).astype(np.uint8)).cuda())
+    ref = {k: v.clone() for k, v in env.build_obs().items()}
+    shapes = {k: tuple(v.shape) for k, v in ref.items()}
+    for lead in (1, 2, 3):
+        for b, n in ((0, E), (5, 20), (36, 1)):
+            out, raw = {}, {}
+            for k, shp in shapes.items():
+                cnt = int(np.prod((n,) + shp[1:]))
+                buf = torch.full((lead + cnt + 5,), -7.0, dtype=torch.float32, device="cuda")
+                raw[k] = buf
+                out[k] = buf[lead:lead + cnt].view((n,) + shp[1:])
+            env.build_obs(env_begin=b, n=n, out=out)
+            torch.cuda.synchronize()
+            for k in shapes:
+                got = out[k].cpu().numpy()
+                want = ref[k][b:b + n].cpu().numpy()
+                assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (k, lead, b, n)
+                r = raw[k].cpu().numpy()
+                assert (r[:lead] == -7.0).all() and (r[lead + got.size:] == -7.0).all(), (k, lead, b, n)
+    # one tensor alone (the others not requested)
+    o = env.build_obs(which=("critic_vec",))
+    assert torch.equal(o["critic_vec"], ref["critic_vec"])
+    env.close()

@@ -118,18 +118,9 @@ struct MdlEngine {
     std::vector<void*> allocs;
     size_t lds_step = 0, lds_obs = 0;
     int wpb_step = 1, wpb_obs = 1;
-    int obs_max_blocks = 0;   // > 0: the small builder's grid cap (its waves loop over envs)
     int n_cu = 0;   // compute units of the device (step_wpb)
     int maxHW = 0;
     bool seeded = false;
-    std::vector<uint8_t> env_map_h;   // [E] map of each env (empty: every env runs map 0)
-    uint32_t* obs_rec = nullptr;      // [E][obs_rec_words] observation records (small builder, MDL_OBS_RECORD)
-    int obs_rec_words = 0;
-    // cells of env e's map (an observation launch covers one same-shape run)
-    int hw_of(int e) const {
-        const int m = env_map_h.empty() ? 0 : env_map_h[e];
-        return mapH[m] * mapW[m];
-    }
     uint64_t map_fp = 0;  // FNV-1a of every map's (H, W, cells, env_map): checkpoint compatibility
     uint64_t cfg_fp = 0;  // FNV-1a of the reward / shaping constants and observation dims: checkpoint compatibility
     // shape_run_end[e]: end (exclusive) of env e's run of consecutive envs whose maps share one
@@ -439,21 +430,7 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     p.obs_small = mdl::obs_use_small((int)A, (int)P, p.key7_dsh, eng->maxHW, p.MO, p.MP) && !getenv("MDL_OBS_GENERIC");
     eng->lds_obs = p.obs_small ? mdl::obs_lds_small((int)A, eng->maxHW, (int)P, p.MO, p.MP)
                                : mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MO, p.MP, p.MR, p.MPs);
-    eng->env_map_h = em;
-    if (p.obs_small && MDL_OBS_RECORD) {
-        // one record per env for the decoupled emission (sized for the largest map's layout)
-        for (int m = 0; m < n_maps; m++)
-            eng->obs_rec_words = std::max(eng->obs_rec_words, mdl::obs_rec_words((int)A, eng->mapH[m] * eng->mapW[m],
-                                                                                 (int)P, p.MO, p.MP, p.MR, p.MPs));
-        if (eng->alloc(&eng->obs_rec, (size_t)c.n_envs * eng->obs_rec_words)) {
-            delete eng;
-            return -1;
-        }
-        eng->lds_obs = mdl::obs_lds_rec(eng->maxHW);
-    }
     eng->wpb_obs = waves_per_block(eng->lds_obs);
-    if (const char* v = getenv("MDL_OBS_BPC"))   // workgroups per CU of the small builder (0 = one wave per env)
-        eng->obs_max_blocks = atoi(v) > 0 ? atoi(v) * std::max(eng->n_cu, 1) : 0;
     if (const char* v = getenv("MDL_OBS_WPB")) {   // profiling override (1..4 waves per workgroup)
         const int x = atoi(v);
         if (x >= 1 && x < eng->wpb_obs) eng->wpb_obs = x;
@@ -545,15 +522,13 @@ int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, 
         if (lds <= LDS_BUDGET) {   // else: the two-launch path below
             const int wpb = step_wpb(E, eng->n_cu, lds, eng->p.P);
             HIPCHK(mdl::launch_step_obs(eng->p, actions, action_format, E, auto_reset, r_env, r_shaped, done,
-                                        actor_map, actor_vec, critic_map, critic_vec, eng->obs_rec, eng->hw_of(0),
-                                        wpb, lds, s));
+                                        actor_map, actor_vec, critic_map, critic_vec, wpb, lds, s));
             return 0;
         }
     }
     HIPCHK(mdl::launch_step(eng->p, actions, action_format, nullptr, E, auto_reset, r_env, r_shaped, done,
                             step_wpb(E, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, s));
-    HIPCHK(mdl::launch_obs(eng->p, 0, E, actor_map, actor_vec, critic_map, critic_vec, eng->obs_rec, eng->hw_of(0),
-                           eng->wpb_obs, eng->lds_obs, s, eng->obs_max_blocks));
+    HIPCHK(mdl::launch_obs(eng->p, 0, E, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs, eng->lds_obs, s));
     return 0;
 }
 
@@ -892,9 +867,8 @@ int mdl_build_obs(MdlEngine* eng, int32_t env_begin, int32_t n, float* actor_map
         return fail("mdl_build_obs: envs [%d, %d) mix map shapes (same-shape run ends at %d)", env_begin,
                     env_begin + n, eng->shape_run_end[env_begin]);
     DeviceGuard dg(eng->device);
-    HIPCHK(mdl::launch_obs(eng->p, env_begin, n, actor_map, actor_vec, critic_map, critic_vec, eng->obs_rec,
-                           eng->hw_of(env_begin), eng->wpb_obs,
-                           eng->lds_obs, (hipStream_t)stream, eng->obs_max_blocks));
+    HIPCHK(mdl::launch_obs(eng->p, env_begin, n, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs,
+                           eng->lds_obs, (hipStream_t)stream));
     return 0;
 }
 

@@ -22,7 +22,6 @@
 #include "mdl_kernels.hpp"
 #include "mdl_features.hpp"
 #include "mdl_obs_small.hpp"
-#include "mdl_obs_expand.hpp"
 #include "mdl_altfeat.hpp"
 
 // Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
@@ -53,11 +52,6 @@
 // path cost more than the reductions they replace (config 2 4.48 -> 4.60 us, measured)
 #ifndef MDL_NEAR_LDS
 #define MDL_NEAR_LDS 1
-#endif
-// ... and there, keys by one v_sad_u16 per candidate plus a start-cell bitmap for the can-pick-up
-// test (maps <= 64 x 64, P <= 128)
-#ifndef MDL_NEAR_SAD16
-#define MDL_NEAR_SAD16 1
 #endif
 #ifndef MDL_ABLATE
 #define MDL_ABLATE 0
@@ -399,8 +393,6 @@ struct ObsArgs {
     float* avec;
     float* cmap;
     float* cvec;
-    uint32_t* rec;   // OBS == 2: the per-env records (row w = env e), expanded by k_obs_expand
-    ObsRec L;
 };
 
 // the completion tail of a Publish launch (every wave of the grid runs it, or the `expect`
@@ -446,8 +438,7 @@ __host__ __device__ constexpr uint64_t move_lt_lanes(int k) {
     return m;
 }
 
-// OBS: 0 none, 1 the small builder's outputs (obs_small_emit), 2 its records (obs_small_record)
-template <bool STALE, int NCH, bool FUSED, int AU, int OBS, bool MAIL = false>
+template <bool STALE, int NCH, bool FUSED, int AU, bool OBS, bool MAIL = false>
 __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, const uint64_t* __restrict__ pkg_pre,
                                           const uint16_t* __restrict__ pst_pre, const u32x4* __restrict__ es_pre,
                                           const uint64_t* __restrict__ trk_pre, const uint8_t* __restrict__ act_pre,
@@ -882,114 +873,61 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                     constexpr int AP = AU <= 8 ? 8 : 16, LG = AU <= 8 ? 3 : 4;
                     uint64_t* cand = (uint64_t*)(smem + (size_t)wave * lds_stride);
                     constexpr int GS = 64 / AP;   // lane groups = candidates per scan step
-                    const MapDesc& mdn = p.maps[mi];
-                    if (MDL_NEAR_SAD16 && NCH <= 2 && mdn.H <= 64 && mdn.W <= 64) {
-                        // Keys by one v_sad_u16 per candidate: cells as (r * 512 | c * 512 << 16), the
-                        // accumulator operand the candidate's order key mapped to 8 bits (survivor rank
-                        // < P <= 128, or 128 + slot), so sad = 512 * distance + ok8 orders like
-                        // (distance, dict order); the winner's start cell comes from an ok8 -> cell
-                        // table, and "a waiting package starts at my new cell" from a 4096-bit map of
-                        // the candidates' start cells (one LDS read per agent instead of a compare
-                        // per candidate).  2 VALU per candidate instead of 4.
-                        uint16_t* okcell = (uint16_t*)(cand + 144);   // [256] ok8 -> start cell
-                        uint32_t* wsb = (uint32_t*)(okcell + 256);    // [128] start-cell bitmap
-                        auto bit_of = [](int cl) { return ((cl & 63) << 6) | ((cl >> 8) & 63); };
-                        auto scaled = [](int cl) { return ((uint32_t)(cl & 0xff) << 9) | ((uint32_t)((cl >> 8) & 0xff) << 25); };
-                        reinterpret_cast<uint2*>(wsb)[lane] = uint2{0u, 0u};
-                        wave_sync();
-                        int nw = 0;
+                    int nw = 0;
 #pragma unroll
-                        for (int c = 0; c < NCH; c++) {
-                            const int idx = nw + popc64(wvm[c] & lanemask_lt());
-                            if (wv[c]) {
-                                const uint32_t ok = tq[c] >= ORD_EPISODE ? 128u + (tq[c] - ORD_EPISODE) : tq[c];
-                                cand[idx] = (uint64_t)scaled(stc[c]) | ((uint64_t)ok << 32);
-                                okcell[ok] = (uint16_t)stc[c];
-                                const int ix = bit_of(stc[c]);
-                                atomicOr(&wsb[ix >> 5], 1u << (ix & 31));
-                            }
-                            nw += popc64(wvm[c]);
-                        }
-                        // sentinels: cell 0, accumulator 0x7fffffff (above every real key, no wrap)
-                        const int nwg = (nw + 2 * GS - 1) & ~(2 * GS - 1);
-                        if (lane < nwg - nw) cand[nw + lane] = 0x7fffffffull << 32;
-                        wave_sync();
-                        const int grp = lane >> LG;
-                        const uint32_t pa = scaled(__builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, pcell));
-                        const uint64_t* cp = cand + grp;
-                        uint32_t kmin = 0xffffffffu;
-                        for (int i0 = 0; i0 < nwg; i0 += 2 * GS) {   // wave-uniform trip count
-                            const uint64_t ce = cp[i0], cf = cp[i0 + GS];
-                            const uint32_t ke = __builtin_amdgcn_sad_u16(pa, (uint32_t)ce, (uint32_t)(ce >> 32));
-                            const uint32_t kf = __builtin_amdgcn_sad_u16(pa, (uint32_t)cf, (uint32_t)(cf >> 32));
-                            kmin = min(kmin, min(ke, kf));
-                        }
-                        uint32_t o = xor_lane<16>(kmin);
-                        kmin = o < kmin ? o : kmin;
-                        o = xor_lane<32>(kmin);
-                        kmin = o < kmin ? o : kmin;
-                        const int ix = bit_of(cell);
-                        Mcan = lmask(act && ((wsb[ix >> 5] >> (ix & 31)) & 1u));
-                        const bool found = act && kmin < 0x7fffffffu;
-                        Midle = lmask(found && (kmin >> 9) <= 3u);
-                        best_cell = found ? (int)okcell[kmin & 255u] : -1;
-                    } else {
-                        int nw = 0;
-#pragma unroll
-                        for (int c = 0; c < NCH; c++) {
-                            const int idx = nw + popc64(wvm[c] & lanemask_lt());
-                            if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo[c] << 32);
-                            nw += popc64(wvm[c]);
-                        }
-                        // sentinels up to a multiple of 2 GS (key bits ~0: never below a real key;
-                        // cell ~0: no map cell), so the scan needs no bound per candidate and
-                        // takes two candidates per lane and step (two LDS reads in flight)
-                        const int nwg = (nw + 2 * GS - 1) & ~(2 * GS - 1);
-                        if (lane < nwg - nw) cand[nw + lane] = ~0ull;
-                        wave_sync();
-                        const int grp = lane >> LG;
-                        const int pa = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, pcell);
-                        // the same scan answers "a waiting package starts at my (new) cell" for
-                        // the can-pick-up test: one compare per candidate into a lane mask (the
-                        // OR over candidates on the scalar unit)
-                        const int ca = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, cell);
-                        const uint64_t* cp = cand + grp;
-                        uint32_t kmin = 0xffffffffu;
-                        uint64_t hm = 0;
-                        for (int i0 = 0; i0 < nwg; i0 += 2 * GS) {   // wave-uniform trip count
-                            const uint64_t ce = cp[i0], cf = cp[i0 + GS];
-                            const uint32_t ke = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
-                            const uint32_t kf = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
-                            kmin = min(kmin, min(ke, kf));
-                            hm |= ballot((int)(uint32_t)ce == ca) | ballot((int)(uint32_t)cf == ca);
-                        }
-                        uint32_t o;
-                        if constexpr (AP == 8) {
-                            o = xor_lane<8>(kmin);
-                            kmin = o < kmin ? o : kmin;
-                        }
-                        o = xor_lane<16>(kmin);
-                        kmin = o < kmin ? o : kmin;
-                        o = xor_lane<32>(kmin);
-                        kmin = o < kmin ? o : kmin;
-                        // agent a's hit: bit a of the lane groups' masks ORed (AP = 16 here)
-                        static_assert(AP == 16, "the hit fold assumes four groups of 16 lanes");
-                        const uint64_t h16 = (hm | (hm >> 16) | (hm >> 32) | (hm >> 48)) & 0xffffull;
-                        // Mcan matters only on lanes with op 1 and no package before or after
-                        // (Mwpick below), i.e. exactly where the per-agent loop would set it
-                        Mcan = sel64(h16, 0u, ~0u);
-                        // the nearest candidate's start cell, from its slot's lane
-                        const int js = (int)(kmin & 1023u);
-                        int bc = __builtin_amdgcn_ds_bpermute((js & 63) << 2, stc[0]);
-#pragma unroll
-                        for (int c = 1; c < NCH; c++) {
-                            const int v = __builtin_amdgcn_ds_bpermute((js & 63) << 2, stc[c]);
-                            bc = (js >> 6) == c ? v : bc;
-                        }
-                        const bool found = act && kmin != 0xffffffffu;
-                        Midle = lmask(found && (kmin >> 21) <= 3u);
-                        best_cell = found ? bc : -1;
+                    for (int c = 0; c < NCH; c++) {
+                        const int idx = nw + popc64(wvm[c] & lanemask_lt());
+                        if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo[c] << 32);
+                        nw += popc64(wvm[c]);
                     }
+                    // sentinels up to a multiple of 2 GS (key bits ~0: never below a real key;
+                    // cell ~0: no map cell), so the scan needs no bound per candidate and
+                    // takes two candidates per lane and step (two LDS reads in flight)
+                    const int nwg = (nw + 2 * GS - 1) & ~(2 * GS - 1);
+                    if (lane < nwg - nw) cand[nw + lane] = ~0ull;
+                    wave_sync();
+                    const int grp = lane >> LG;
+                    const int pa = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, pcell);
+                    // the same scan answers "a waiting package starts at my (new) cell" for
+                    // the can-pick-up test: one compare per candidate into a lane mask (the
+                    // OR over candidates on the scalar unit)
+                    const int ca = __builtin_amdgcn_ds_bpermute((lane & (AP - 1)) << 2, cell);
+                    const uint64_t* cp = cand + grp;
+                    uint32_t kmin = 0xffffffffu;
+                    uint64_t hm = 0;
+                    for (int i0 = 0; i0 < nwg; i0 += 2 * GS) {   // wave-uniform trip count
+                        const uint64_t ce = cp[i0], cf = cp[i0 + GS];
+                        const uint32_t ke = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
+                        const uint32_t kf = ((uint32_t)manhattan_sad(pa, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
+                        kmin = min(kmin, min(ke, kf));
+                        hm |= ballot((int)(uint32_t)ce == ca) | ballot((int)(uint32_t)cf == ca);
+                    }
+                    uint32_t o;
+                    if constexpr (AP == 8) {
+                        o = xor_lane<8>(kmin);
+                        kmin = o < kmin ? o : kmin;
+                    }
+                    o = xor_lane<16>(kmin);
+                    kmin = o < kmin ? o : kmin;
+                    o = xor_lane<32>(kmin);
+                    kmin = o < kmin ? o : kmin;
+                    // agent a's hit: bit a of the lane groups' masks ORed (AP = 16 here)
+                    static_assert(AP == 16, "the hit fold assumes four groups of 16 lanes");
+                    const uint64_t h16 = (hm | (hm >> 16) | (hm >> 32) | (hm >> 48)) & 0xffffull;
+                    // Mcan matters only on lanes with op 1 and no package before or after
+                    // (Mwpick below), i.e. exactly where the per-agent loop would set it
+                    Mcan = sel64(h16, 0u, ~0u);
+                    // the nearest candidate's start cell, from its slot's lane
+                    const int js = (int)(kmin & 1023u);
+                    int bc = __builtin_amdgcn_ds_bpermute((js & 63) << 2, stc[0]);
+#pragma unroll
+                    for (int c = 1; c < NCH; c++) {
+                        const int v = __builtin_amdgcn_ds_bpermute((js & 63) << 2, stc[c]);
+                        bc = (js >> 6) == c ? v : bc;
+                    }
+                    const bool found = act && kmin != 0xffffffffu;
+                    Midle = lmask(found && (kmin >> 21) <= 3u);
+                    best_cell = found ? bc : -1;
                     q = 0;
                 }
                 if constexpr (NCH == 1) {
@@ -1181,12 +1119,9 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
     if (lane == 0)
         for (int k = 0; k < 16; k++) g_stamps[(size_t)w * 16 + k] = stamp_[k];
 #endif
-    if constexpr (OBS == 1)   // full batch only (no env_ids): output row w = env e
+    if constexpr (OBS)   // full batch only (no env_ids): output row w = env e
         obs_small_emit<STALE>(p, w, mi, act ? rob_pack(cell, carry, vmask) : 0u, pk[0], ps[0], STALE ? td[0] : 0ull,
                               t_cur, oa.amap, oa.avec, oa.cmap, oa.cvec, smem + (size_t)wave * lds_stride);
-    if constexpr (OBS == 2)
-        obs_small_record<STALE>(p, mi, act ? rob_pack(cell, carry, vmask) : 0u, pk[0], ps[0], STALE ? td[0] : 0ull,
-                                t_cur, oa.L, oa.rec + (size_t)w * oa.L.words, smem + (size_t)wave * lds_stride);
     if constexpr (MAIL) {   // row w of the call: k_mail_export's layout, from the registers
         const MailRows& m = ma->m;
         if (act) {
@@ -1222,7 +1157,7 @@ __global__ __launch_bounds__(MDL_STEP_LB) MDL_STEP_ATTR(NCH, FUSED) void k_step(
                                                       const uint64_t* __restrict__ trk_pre,
                                                       const uint8_t* __restrict__ act_pre, uint32_t ap,
                                                       uint32_t nw, StepArgs args) {
-    step_body<STALE, NCH, FUSED, AU, 0>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre, act_pre, ap, nw, args,
+    step_body<STALE, NCH, FUSED, AU, false>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre, act_pre, ap, nw, args,
                                             ObsArgs{});
 }
 
@@ -1236,13 +1171,12 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step_mail(const uint32_t* __res
                                                            const uint64_t* __restrict__ trk_pre,
                                                            const uint8_t* __restrict__ act_pre, uint32_t ap,
                                                            uint32_t nw, StepArgs args, MailArgs ma, int inl) {
-    step_body<STALE, NCH, false, AU, 0, true>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre,
+    step_body<STALE, NCH, false, AU, false, true>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre,
                                                   inl ? ma.codes : act_pre, ap, nw, args, ObsArgs{}, &ma);
 }
 
-// mdl_step_obs: k_step + k_obs_small in one launch (full batch, NCH = 1, A <= 8); OBS = 2: the
-// observations' records, expanded by a k_obs_expand launch behind it
-template <bool STALE, int AU, int OBS>
+// mdl_step_obs: k_step + k_obs_small in one launch (full batch, NCH = 1, A <= 8)
+template <bool STALE, int AU>
 __global__ __launch_bounds__(256) MDL_STEP_ATTR(1, false) void k_step_obs(const uint32_t* __restrict__ rob_pre,
                                                   const uint64_t* __restrict__ pkg_pre,
                                                   const uint16_t* __restrict__ pst_pre,
@@ -1250,7 +1184,7 @@ __global__ __launch_bounds__(256) MDL_STEP_ATTR(1, false) void k_step_obs(const 
                                                   const uint64_t* __restrict__ trk_pre,
                                                   const uint8_t* __restrict__ act_pre, uint32_t ap, uint32_t nw,
                                                   StepArgs args, ObsArgs oa) {
-    step_body<STALE, 1, false, AU, OBS>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre, act_pre, ap, nw, args, oa);
+    step_body<STALE, 1, false, AU, true>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre, act_pre, ap, nw, args, oa);
 }
 
 // ------------------------------------------------------------- observations
@@ -1930,60 +1864,11 @@ hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, cons
     return hipGetLastError();
 }
 
-// The flat emission pass over the records of output rows [0, n) (mdl_obs_expand.hpp): one launch
-// per chunk of envs whose every segment stays below 2^31 floats (the magic divisions' range).
-hipError_t launch_obs_expand(const DevParams& p, int HW, int n, const uint32_t* recs, float* amap, float* avec,
-                             float* cmap, float* cvec, hipStream_t s) {
-    const int A = p.A;
-    const ObsRec L = obs_rec_layout(A, HW, p.P, p.MO, p.MP, p.MR, p.MPs);
-    ExpandArgs x{};
-    x.L = L;
-    x.A = A;
-    x.HW = HW;
-    x.np = 6 * A;
-    x.Dv = 6 + 5 * p.MO + 5 * p.MP + 1;
-    x.ps0 = 6 + 5 * p.MO;
-    x.Dg = 6 * p.MR + 7 * p.MPs + 1;
-    x.MR6 = 6 * p.MR;
-    if (HW < 2) return hipErrorInvalidValue;
-    x.mHW = obs_magic((uint32_t)HW);
-    x.mDv = obs_magic((uint32_t)x.Dv);
-    float* outs[4] = {amap, cmap, avec, cvec};
-    const uint64_t D[4] = {6ull * A * HW, 4ull * HW, (uint64_t)A * x.Dv, (uint64_t)x.Dg};
-    uint64_t dmax = 1;
-    for (int k = 0; k < 4; k++)
-        if (outs[k] && D[k] > dmax) dmax = D[k];
-    if (dmax >= (1ull << 31)) return hipErrorInvalidValue;
-    const int chunk = (int)std::min<uint64_t>((uint64_t)n, ((1ull << 31) - 1) / dmax);
-    for (int e0 = 0; e0 < n; e0 += chunk) {
-        const int m = std::min(chunk, n - e0);
-        x.rec = recs + (size_t)e0 * L.words;
-        uint32_t blk = 0;
-        for (int k = 0; k < 4; k++) {
-            ExpSeg& S = x.seg[k];
-            S = ExpSeg{};
-            S.blk0 = blk;
-            if (!outs[k]) continue;
-            float* base = outs[k] + (size_t)e0 * D[k];
-            S.lead = (uint32_t)(((uintptr_t)base & 15u) >> 2);
-            S.out = base - S.lead;
-            S.D = (uint32_t)D[k];
-            S.nf = (uint32_t)(D[k] * (uint64_t)m);
-            S.mD = obs_magic(S.D);
-            blk += (S.lead + S.nf + 1023u) / 1024u;
-        }
-        if (blk == 0) return hipSuccess;
-        hipLaunchKernelGGL(k_obs_expand, dim3(blk), dim3(256), 0, s, x);
-    }
-    return hipGetLastError();
-}
-
 // k_step_obs (mdl_step_obs): full batch, NCH = 1, A <= 8, the small observation builder;
-// lds = the per-wave slice (max of the step's reset scratch and the builder's LDS); with records
-// (recs != nullptr) the step writes each env's record and k_obs_expand follows it
+// lds = the per-wave slice (max of the step's reset scratch and the builder's planes)
 hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
-                           float* sh, uint8_t* done, float* amap, float* avec, float* cmap, float* cvec,
-                           uint32_t* recs, int HW, int wpb, size_t lds, hipStream_t s) {
+                           float* sh, uint8_t* done, float* amap, float* avec, float* cmap, float* cvec, int wpb,
+                           size_t lds, hipStream_t s) {
     if (nch_for(p.P) != 1 || p.A > 8 || !p.obs_small) return hipErrorInvalidValue;
     StepArgs a;
     a.p = p;
@@ -1998,33 +1883,20 @@ hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, 
     a.wpb = wpb;
     a.lds_stride = (int)lds;
     a.K = 1;
-    ObsArgs o{amap, avec, cmap, cvec, recs, {}};
-    if (recs) o.L = obs_rec_layout(p.A, HW, p.P, p.MO, p.MP, p.MR, p.MPs);
+    const ObsArgs o{amap, avec, cmap, cvec};
     const dim3 grid(blocks_for(n, wpb)), block(64 * wpb);
     const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a, o
-#define MDL_STEP_OBS(ST, AU)                                                                         \
-    do {                                                                                             \
-        if (recs) hipLaunchKernelGGL((k_step_obs<ST, AU, 2>), grid, block, lds * wpb, s, MDL_STEP_ARGS); \
-        else hipLaunchKernelGGL((k_step_obs<ST, AU, 1>), grid, block, lds * wpb, s, MDL_STEP_ARGS);      \
-    } while (0)
     if (p.stale) {
-        if (p.A == 5) MDL_STEP_OBS(true, 5);
-        else MDL_STEP_OBS(true, 8);
+        if (p.A == 5) hipLaunchKernelGGL((k_step_obs<true, 5>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+        else hipLaunchKernelGGL((k_step_obs<true, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
     } else {
-        if (p.A == 5) MDL_STEP_OBS(false, 5);
-        else MDL_STEP_OBS(false, 8);
+        if (p.A == 5) hipLaunchKernelGGL((k_step_obs<false, 5>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+        else hipLaunchKernelGGL((k_step_obs<false, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
     }
-#undef MDL_STEP_OBS
 #undef MDL_STEP_ARGS
-    if (recs) return launch_obs_expand(p, HW, n, recs, amap, avec, cmap, cvec, s);
     return hipGetLastError();
-}
-
-size_t obs_lds_rec(int HW) { return obs_rec_lds(HW); }
-int obs_rec_words(int A, int HW, int P, int MO, int MP, int MR, int MPs) {
-    return obs_rec_layout(A, HW, P, MO, MP, MR, MPs).words;
 }
 
 size_t alt_obs_lds(int P, int HW) { return obs_pre_bytes(P) + alt_lds_bytes(HW); }
@@ -2067,26 +1939,14 @@ hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt
 }
 
 hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
-                      uint32_t* recs, int HW, int wpb, size_t lds, hipStream_t s, int max_blocks) {
-    if (p.obs_small && recs) {   // records, then the flat emission pass
-        const ObsRec L = obs_rec_layout(p.A, HW, p.P, p.MO, p.MP, p.MR, p.MPs);
-        if (p.stale)
-            hipLaunchKernelGGL(k_obs_small_rec<true>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin,
-                               n, L, recs, wpb, (int)lds);
-        else
-            hipLaunchKernelGGL(k_obs_small_rec<false>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p,
-                               env_begin, n, L, recs, wpb, (int)lds);
-        return launch_obs_expand(p, HW, n, recs, amap, avec, cmap, cvec, s);
-    }
+                      int wpb, size_t lds, hipStream_t s) {
     if (p.obs_small) {
-        int nb = blocks_for(n, wpb);
-        if (max_blocks > 0 && nb > max_blocks) nb = max_blocks;
         if (p.stale)
-            hipLaunchKernelGGL(k_obs_small<true>, dim3(nb), dim3(256), lds * wpb, s, p, env_begin, n, amap, avec, cmap,
-                               cvec, wpb, (int)lds);
+            hipLaunchKernelGGL(k_obs_small<true>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin, n,
+                               amap, avec, cmap, cvec, wpb, (int)lds);
         else
-            hipLaunchKernelGGL(k_obs_small<false>, dim3(nb), dim3(256), lds * wpb, s, p, env_begin, n, amap, avec,
-                               cmap, cvec, wpb, (int)lds);
+            hipLaunchKernelGGL(k_obs_small<false>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin,
+                               n, amap, avec, cmap, cvec, wpb, (int)lds);
         return hipGetLastError();
     }
     if (p.stale)

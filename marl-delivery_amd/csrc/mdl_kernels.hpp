@@ -19,24 +19,11 @@ hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, cons
 hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int K,
                              int auto_reset, double* r, float* sh, uint8_t* done, int wpb, size_t lds,
                              hipStream_t s);
-// Observations of the small builder through per-env records + the flat emission pass
-// (mdl_obs_expand.hpp) when recs != nullptr (records of rows [0, n), HW = the launch's map cells);
-// otherwise the wave-per-env builder writes the outputs itself.
-// (measured slower than the wave-per-env builder: profiles/r04/obs_record_vs_slab_ab.txt -- off)
-#ifndef MDL_OBS_RECORD
-#define MDL_OBS_RECORD 0
-#endif
 hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
-                           float* sh, uint8_t* done, float* amap, float* avec, float* cmap, float* cvec,
-                           uint32_t* recs, int HW, int wpb, size_t lds, hipStream_t s);
-// max_blocks > 0: at most that many workgroups; the small builder's waves then loop over envs
-// (each wave's stores of one env drain while it computes the next)
+                           float* sh, uint8_t* done, float* amap, float* avec, float* cmap, float* cvec, int wpb,
+                           size_t lds, hipStream_t s);
 hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
-                      uint32_t* recs, int HW, int wpb, size_t lds, hipStream_t s, int max_blocks = 0);
-hipError_t launch_obs_expand(const DevParams& p, int HW, int n, const uint32_t* recs, float* amap, float* avec,
-                             float* cmap, float* cvec, hipStream_t s);
-size_t obs_lds_rec(int HW);
-int obs_rec_words(int A, int HW, int P, int MO, int MP, int MR, int MPs);
+                      int wpb, size_t lds, hipStream_t s);
 // A launch's own completion word (host-mapped): every wave of its grid counts itself in the
 // running device counter `ctr` (never reset: `base` is its value before the launch) after a
 // system-scope release of its stores; the last one writes `value` to `seq`.  seq == nullptr: none;

@@ -38,12 +38,9 @@
 #ifndef MDL_OBS_SINGLEWRITE
 #define MDL_OBS_SINGLEWRITE 1
 #endif
-// The map planes (two thirds of config 3's bytes, no global loads) emitted after the vectors: a
-// wave's global loads (the rank table gathers of the package order and of the other-robot order)
-// then all come before its first store -- vmcnt counts stores too, so a load issued behind the
-// map planes' stores waited for them to drain before the vector work could go on.
-#ifndef MDL_OBS_MAPS_LAST
-#define MDL_OBS_MAPS_LAST 1
+// Package order for a few slots by all agents' minima at once (wave_min8_u32)
+#ifndef MDL_OBS_MIN8
+#define MDL_OBS_MIN8 1
 #endif
 
 namespace mdl {
@@ -390,37 +387,33 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
     if (pres) o2j[ord7] = (uint8_t)lane;
     wave_sync();
 
-    // ---- maps (a lambda: emitted after the vectors, see MDL_OBS_MAPS_LAST) ----
-    auto obs_maps = [&]() {
-        float* am = amap ? amap + (size_t)w * A * 6 * HW : nullptr;
-        float* cm = cmap ? cmap + (size_t)w * 4 * HW : nullptr;
-        if (am) {
-            // plane p = (agent p/6, channel p%6): grid, self, other robots, waiting starts,
-            // active targets, own carried target (MAPPO/helper.py:6-66)
-            build_flat(planes, 6 * A, HW, [&](int pp, int c0) -> uint32_t {
-                const int a = pp / 6, ch = pp - 6 * a;
-                const int bs = ch == 0 ? BS_GRID : ch == 3 ? BS_WSTART : ch == 4 ? BS_ATARGET : BS_ROBOT;
-                const uint32_t so = onehot32(aidx[2 * a], c0), to = onehot32(aidx[2 * a + 1], c0);
-                uint32_t v = bits_at(bits, NW, bs, c0);
-                v = ch == 2 ? (v & ~so) | bits_at(bits, NW, BS_MULTI, c0) : v;
-                return ch == 1 ? so : ch == 5 ? to : v;
-            });
-        }
-        if (cm)   // critic planes = bitsets 0..3 (grid, robots, waiting starts, active targets)
-            build_flat(cplanes, 4, HW, [&](int pp, int c0) -> uint32_t { return bits_at(bits, NW, pp, c0); });
-        wave_sync();
-        if (am) {
-            if (((uintptr_t)am & 15) == 0) emit_flat4(planes, 6 * A * HW, am);
-            else emit_flat1(planes, 6 * A * HW, am);
-        }
-        if (cm) {
-            if (((uintptr_t)cm & 15) == 0) emit_flat4(cplanes, 4 * HW, cm);
-            else emit_flat1(cplanes, 4 * HW, cm);
-        }
-    };
-#if !MDL_OBS_MAPS_LAST
-    obs_maps();
-#endif
+    // ---- maps ----
+    float* am = amap ? amap + (size_t)w * A * 6 * HW : nullptr;
+    float* cm = cmap ? cmap + (size_t)w * 4 * HW : nullptr;
+    if (am) {
+        // plane p = (agent p/6, channel p%6): grid, self, other robots, waiting starts,
+        // active targets, own carried target (MAPPO/helper.py:6-66)
+        build_flat(planes, 6 * A, HW, [&](int pp, int c0) -> uint32_t {
+            const int a = pp / 6, ch = pp - 6 * a;
+            const int bs = ch == 0 ? BS_GRID : ch == 3 ? BS_WSTART : ch == 4 ? BS_ATARGET : BS_ROBOT;
+            const uint32_t so = onehot32(aidx[2 * a], c0), to = onehot32(aidx[2 * a + 1], c0);
+            uint32_t v = bits_at(bits, NW, bs, c0);
+            v = ch == 2 ? (v & ~so) | bits_at(bits, NW, BS_MULTI, c0) : v;
+            return ch == 1 ? so : ch == 5 ? to : v;
+        });
+    }
+    if (cm)   // critic planes = bitsets 0..3 (grid, robots, waiting starts, active targets)
+        build_flat(cplanes, 4, HW, [&](int pp, int c0) -> uint32_t { return bits_at(bits, NW, pp, c0); });
+    wave_sync();
+    if (am) {
+        if (((uintptr_t)am & 15) == 0) emit_flat4(planes, 6 * A * HW, am);
+        else emit_flat1(planes, 6 * A * HW, am);
+    }
+    if (cm) {
+        if (((uintptr_t)cm & 15) == 0) emit_flat4(cplanes, 4 * HW, cm);
+        else emit_flat1(cplanes, 4 * HW, cm);
+    }
+
     // ---- actor vectors (MAPPO/helper.py:68-165) ----
     if (avec) {
         const int Dv = 6 + 5 * MO + 5 * MP + 1;
@@ -448,6 +441,25 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
 #pragma unroll
             for (int a = 0; a < 5; a++)
                 if (lane < want) invp[a * 64 + lane] = o2j[k5[a] & 127u];
+        } else if (want <= 6 && MDL_OBS_MIN8) {
+            // a few slots: repeated wave minima (keys are unique), all agents' at once by the
+            // halving transpose (wave_min8_u32: ~20 VALU per slot for every agent instead of a
+            // 6-stage DPP chain per agent)
+            for (int s = 0; s < want; s++) {
+                uint32_t k8[8];
+#pragma unroll
+                for (int a = 0; a < 8; a++) k8[a] = a < A ? key[a] : 0xffffffffu;
+                const uint32_t v = wave_min8_u32(k8);
+#pragma unroll
+                for (int a = 0; a < 8; a++) {
+                    if (a < A) {
+                        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)v, wave_min8_lane(a));
+                        const bool hit = key[a] == m;
+                        if (hit) invp[a * 64 + s] = (uint8_t)lane;
+                        key[a] = hit ? 0xffffffffu : key[a];
+                    }
+                }
+            }
         } else if (want <= 6) {
             // a few slots: repeated wave minima (keys are unique)
             for (int s = 0; s < want; s++) {
@@ -706,316 +718,12 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
         }
         if (lane == 0) cv[Dg - 1] = qdiv_r(t, yT);
     }
-#if MDL_OBS_MAPS_LAST
-    obs_maps();
-#endif
 }
 
-// ---------------------------------------------------------------- decoupled emission
-// The observation outputs are ~20-40 KB per env of float32, mostly 0/1 map planes and padding.
-// A wave-per-env builder streams them as (resident waves) separate write streams, which caps at
-// 5.1-5.3 TB/s on MI355X whatever the per-wave order (profiles/r03/slab_write_shapes*.jsonl); a
-// flat pass in which thread i writes float4 i, blocks in address order, is one chip-wide moving
-// write window (6.3+ TB/s).  So the builder is split: obs_small_record writes a compact record
-// per env (cell bitsets, the agents' cells / carried targets, the vector tuples that can be
-// non-zero, a few counts), and k_obs_expand (mdl_obs_expand.hpp) expands the records into the
-// four output tensors.  Every value is computed exactly as before (same divisions, same tuple
-// lanes); the expansion only places record words and zeros.
-//
-// Record of one env, u32 words (layout shared by host and device):
-//   [0] want: filled package slots per agent    [1] npr: critic package rows
-//   [2] t/T as float bits                       [3] 0
-//   aidx [A][2]: each agent's cell index r*W+c and its carried in-transit target (-1 none)
-//   bits [5][NW]: the cell bitsets (BS_* order: grid, robots, waiting starts, active targets, >= 2 robots)
-//   av   [A][RA]: agent a's self tuple (6), its MOc other-robot tuples (5 each), its first `want`
-//        package tuples (5 each) -- RA = 6 + 5 MOc + 5 MPc
-//   cv   [6 nr + 7 MPsc]: the critic's nr robot rows then its first npr package rows
-struct ObsRec {
-    int words;   // record stride (multiple of 4 words: 16-B aligned records)
-    int o_aidx, o_bits, o_av, o_cv;
-    int NW, RA, nr, MOc;
-};
-__host__ __device__ inline ObsRec obs_rec_layout(int A, int HW, int P, int MO, int MP, int MR, int MPs) {
-    ObsRec L;
-    const int MOc = MO < A - 1 ? MO : A - 1, MPc = MP < P ? MP : P, MPsc = MPs < P ? MPs : P;
-    L.MOc = MOc;
-    L.NW = (HW + 31) / 32;
-    L.RA = 6 + 5 * MOc + 5 * MPc;
-    L.nr = A < MR ? A : MR;
-    L.o_aidx = 4;
-    L.o_bits = (L.o_aidx + 2 * A + 3) & ~3;
-    L.o_av = (L.o_bits + 5 * L.NW + 3) & ~3;
-    L.o_cv = (L.o_av + A * L.RA + 3) & ~3;
-    L.words = (L.o_cv + 6 * L.nr + 7 * MPsc + 3) & ~3;
-    return L;
-}
-// LDS bytes per wave of the record builder: bitsets (5 NW + guard), carrier table and critic order
-// (64 words each), order -> slot map (128 B), package order of each agent (8 x 64 B), agent cells
-// (16 words)
-__host__ __device__ inline size_t obs_rec_lds(int HW) {
-    const int NW = (HW + 31) / 32;
-    return (4 * (size_t)(5 * NW + 1) + 2 * 256 + 128 + 512 + 64 + 15) & ~(size_t)15;
-}
-
-// The record of env e (output row w) from its state words as the lanes hold them (see
-// obs_small_emit: the same inputs, the same values).  `rec` is this env's record.
 template <bool STALE>
-__device__ __forceinline__ void obs_small_record(const DevParams& p, int mi, uint32_t rv, uint64_t pkd, uint32_t f,
-                                                 uint64_t tdd, int t, const ObsRec& L, uint32_t* __restrict__ rec,
-                                                 unsigned char* smem_wave) {
-    const int lane = lane_id();
-    const int A = p.A, P = p.P;
-    const MapDesc md = p.maps[mi];
-    const int H = md.H, W = md.W, HW = H * W, NW = L.NW;
-    const int T = p.obsT, MO = p.MO, MP = p.MP, MPs = p.MPs;
-    const int MPc = MP < P ? MP : P, MPsc = MPs < P ? MPs : P;
-    const int MOc = L.MOc, RA = L.RA;
-    const double yH = p.obs_recip[2 * mi], yW = p.obs_recip[2 * mi + 1];   // RN(1/H), RN(1/W)
-    const double yT = p.obs_recip[2 * p.n_maps], yM = p.obs_recip[2 * p.n_maps + 1];
-    const uint16_t* rank = p.rank + md.rank_off;
-    const int rW = 2 * W - 1, rOff = (H - 1) * rW + (W - 1);   // rank[(dr+H-1)*(2W-1) + dc+W-1]
-    (void)HW;
-
-    uint32_t* bits = (uint32_t*)smem_wave;                       // [5][NW] + guard
-    int* scar = (int*)(bits + 5 * NW + 1);                        // [64] carrier robot of a slot
-    int* invc = scar + 64;                                        // [64] critic row -> slot
-    uint8_t* o2j = (uint8_t*)(invc + 64);                         // [128] 7-bit order -> slot
-    uint8_t* invp = o2j + 128;                                    // [8][64] (agent, rank) -> slot
-
-    const bool rl = lane < A, pl = lane < P;
-    if (lane == 0) bits[5 * NW] = 0;
-    for (int k = lane; k < NW; k += WAVE) {
-        bits[BS_GRID * NW + k] = p.gridbits[md.bits_off + k];
-        bits[BS_ROBOT * NW + k] = 0;
-        bits[BS_MULTI * NW + k] = 0;
-        bits[BS_WSTART * NW + k] = 0;
-        bits[BS_ATARGET * NW + k] = 0;
-    }
-    scar[lane] = 0x7f;
-
-    // ---- tracker view of each slot (as obs_small_emit) ----
-    bool pres, trans;
-    uint64_t dat;
-    uint32_t ord7;
-    if (STALE) {
-        pres = (f & PS_PRESENT) != 0;
-        trans = (f & PS_TRANSIT) != 0;
-        const bool sv = (f & PS_SURVIVOR) != 0;
-        dat = sv ? tdd : pkd;
-        ord7 = sv ? (f >> PS_RANK_SHIFT) & 63u : 64u + (uint32_t)lane;
-    } else {
-        const uint32_t s = f & PS_STATUS;
-        pres = s == ST_WAITING || s == ST_IN_TRANSIT;
-        trans = s == ST_IN_TRANSIT;
-        dat = pkd;
-        ord7 = (uint32_t)lane;
-    }
-    pres = pres && pl;
-    trans = trans && pres;
-    const int scl = pk_start(dat), tgl = pk_target(dat);
-    const int sr = cell_r(scl), sc = cell_c(scl), tr = cell_r(tgl), tc = cell_c(tgl);
-    const int stt = pk_st(dat);
-    const bool wt = pres && !trans && stt <= t;
-    const bool actv = pres && (trans || stt <= t);
-    int dlc = pk_dl(dat) - t;
-    dlc = (dlc < 0 || T <= 0) ? 0 : dlc;
-
-    // ---- robots ----
-    const int cell = rob_cell(rv), carry = rob_carry(rv);
-    const int rr = cell_r(cell), rc = cell_c(cell);
-    const bool cin = rl && carry >= 1 && carry <= P;
-    const int cs = cin ? carry - 1 : 0;
-    const int g_fl = bperm((int)pres | ((int)trans << 1), cs);
-    const int g_tg = bperm(tgl, cs), g_dl = bperm(dlc, cs);
-    const bool ctr = cin && (g_fl & 1) && (g_fl & 2);
-    const int ctr_r = cell_r(g_tg), ctr_c = cell_c(g_tg);
-    const int cidx = rr * W + rc, tidx = ctr ? ctr_r * W + ctr_c : -1;
-
-    // ---- cell bitsets, carriers, critic order, order map ----
-    wave_sync();
-    if (rl) {
-        rec[L.o_aidx + 2 * lane] = (uint32_t)cidx;
-        rec[L.o_aidx + 2 * lane + 1] = (uint32_t)tidx;
-        const uint32_t m = 1u << (cidx & 31);
-        const uint32_t old = atomicOr(&bits[BS_ROBOT * NW + (cidx >> 5)], m);
-        if (old & m) atomicOr(&bits[BS_MULTI * NW + (cidx >> 5)], m);
-        if (carry >= 1 && carry <= WAVE) atomicMin(&scar[carry - 1], lane);
-    }
-    if (wt) {
-        const int ci = sr * W + sc;
-        atomicOr(&bits[BS_WSTART * NW + (ci >> 5)], 1u << (ci & 31));
-    }
-    if (wt || trans) {
-        const int ci = tr * W + tc;
-        atomicOr(&bits[BS_ATARGET * NW + (ci >> 5)], 1u << (ci & 31));
-    }
-    const uint64_t actm = ballot(actv);
-    const int cpos = popc64(actm & lanemask_lt());
-    const int nact = popc64(actm);
-    if (actv) invc[cpos] = lane;
-    if (pres) o2j[ord7] = (uint8_t)lane;
-    const int np = popc64(ballot(wt));
-    const int want = np < MPc ? np : MPc;
-    const int npr = nact < MPsc ? nact : MPsc;
-    wave_sync();
-    for (int k = lane; k < 5 * NW; k += WAVE) rec[L.o_bits + k] = bits[k];
-    if (lane == 0) {
-        rec[0] = (uint32_t)want;
-        rec[1] = (uint32_t)npr;
-        rec[2] = __float_as_uint(qdiv_r(t, yT));   // yT = 0 when T <= 0
-        rec[3] = 0u;
-    }
-
-    // ---- actor vector tuples (MAPPO/helper.py:68-165) ----
-    {
-        float* av = reinterpret_cast<float*>(rec + L.o_av);
-        const int dsh = p.key7_dsh;
-        uint32_t key[8];
-#pragma unroll
-        for (int a = 0; a < 8; a++) {
-            key[a] = 0xffffffffu;
-            if (a < A) {
-                const int ra_ = rdl(rr, a), ca_ = rdl(rc, a);
-                const uint32_t rk = rank[rOff + (sr - ra_) * rW + (sc - ca_)];
-                key[a] = wt ? ((uint32_t)dlc << dsh) | (rk << 7) | ord7 : 0xffffffffu;
-            }
-        }
-        if (A == 5 && want > 6) {
-            uint32_t k5[5];
-#pragma unroll
-            for (int a = 0; a < 5; a++) k5[a] = key[a];
-            sort64_u32xn<5>(k5);
-#pragma unroll
-            for (int a = 0; a < 5; a++)
-                if (lane < want) invp[a * 64 + lane] = o2j[k5[a] & 127u];
-        } else if (want <= 6) {
-            for (int s = 0; s < want; s++) {
-#pragma unroll
-                for (int a = 0; a < 8; a++) {
-                    if (a < A) {
-                        const uint32_t m = wave_min_u32(key[a]);
-                        const bool hit = key[a] == m;
-                        if (hit) invp[a * 64 + s] = (uint8_t)lane;
-                        key[a] = hit ? 0xffffffffu : key[a];
-                    }
-                }
-            }
-        } else {
-#pragma unroll
-            for (int a = 0; a < 8; a++) {
-                if (a < A) {
-                    const uint32_t sk = sort64_u32(key[a]);
-                    if (lane < want) invp[a * 64 + lane] = o2j[sk & 127u];
-                }
-            }
-        }
-        wave_sync();
-        // Tuple lanes: q < A*A other robots (agent q/A, robot q%A), then A*want filled package
-        // slots (agent, slot), then A self tuples (empty slots are zeros of the expansion).
-        const int nq_o = A * A, nq_p = A * want, ntup = nq_o + nq_p + A;
-        const float inv_a = 1.0f / (float)A, inv_w = want > 0 ? 1.0f / (float)want : 0.0f;
-        for (int q0 = 0; q0 < ntup; q0 += WAVE) {   // uniform trip count
-            const int q = q0 + lane;
-            const bool is_o = q < nq_o, is_p = !is_o && q < nq_o + nq_p, is_s = !is_o && !is_p && q < ntup;
-            int qa, qb;
-            if (is_o) {
-                qa = fdivi(q, A, inv_a);
-                qb = q - qa * A;
-            } else if (is_p) {
-                qa = fdivi(q - nq_o, want, inv_w);
-                qb = q - nq_o - qa * want;
-            } else {
-                qa = is_s ? q - nq_o - nq_p : 0;
-                qb = qa;
-            }
-            const int ra = bperm(rr, qa), ca = bperm(rc, qa);
-            const int ob = is_o ? qb : 0;
-            const int ro = bperm(rr, ob), co = bperm(rc, ob);
-            const bool ovalid = is_o && qb != qa;
-            const int orank = rank[rOff + (ro - ra) * rW + (co - ca)];
-            const int okey = ovalid ? (orank << 3) | qb : 0x7fffffff;   // (rank, robot index)
-            int opos = 0;
-            for (int k = 0; k < A; k++) opos += bperm(okey, (qa * A + k) & 63) < okey;
-            const int pj = is_p ? invp[qa * 64 + qb] : 0;
-            const int p_sc = bperm(scl, pj), p_tg = bperm(tgl, pj), p_dl = bperm(dlc, pj);
-            const int rsrc = is_o ? qb : qa;
-            const int o_cy = bperm(carry, rsrc), o_ctr = bperm((int)ctr, rsrc);
-            const int o_tr = bperm(ctr_r, rsrc), o_tc = bperm(ctr_c, rsrc), o_dl = bperm(g_dl, rsrc);
-            int x1, x2, x3, x4, x5;
-            if (is_p) {
-                x1 = cell_r(p_sc) - ra;
-                x2 = cell_c(p_sc) - ca;
-                x3 = cell_r(p_tg) - ra;
-                x4 = cell_c(p_tg) - ca;
-                x5 = p_dl;
-            } else {
-                const int br = is_o ? ro : ra, bc = is_o ? co : ca;
-                x1 = is_o ? ro - ra : ra;
-                x2 = is_o ? co - ca : ca;
-                const bool ht = o_cy != 0 && o_ctr != 0;
-                x3 = ht ? o_tr - br : 0;
-                x4 = ht ? o_tc - bc : 0;
-                x5 = ht ? o_dl : 0;
-            }
-            const float d1 = qdiv_r(x1, yH), d2 = qdiv_r(x2, yW), d3 = qdiv_r(x3, yH), d4 = qdiv_r(x4, yW);
-            const float d5 = qdiv_r(x5, yT);
-            const float fl = o_cy != 0 ? 1.0f : 0.0f;
-            if ((ovalid && opos < MO) || is_p || is_s) {
-                const int off = is_s ? 0 : is_o ? 6 + 5 * opos : 6 + 5 * MOc + 5 * qb;
-                float* o = av + qa * RA + off;
-                o[0] = d1;
-                o[1] = d2;
-                o[2] = is_p ? d3 : fl;
-                o[3] = is_p ? d4 : d3;
-                o[4] = is_p ? d5 : d4;
-                if (is_s) o[5] = d5;
-            }
-        }
-    }
-
-    // ---- critic vector rows (MAPPO/helper.py:199-255) ----
-    {
-        float* cv = reinterpret_cast<float*>(rec + L.o_cv);
-        const int nr = L.nr;
-        for (int q0 = 0; q0 < nr + npr; q0 += WAVE) {   // uniform trip count: bperm needs every lane
-            const int q = q0 + lane;
-            const bool isr = q < nr, live = q < nr + npr;
-            const int j = (isr || !live) ? 0 : invc[q - nr];
-            const int p_sc = bperm(scl, j), p_tg = bperm(tgl, j), p_dl = bperm(dlc, j);
-            const int p_tr = bperm((int)trans, j), p_car = scar[j];
-            const int rq = q & 63;
-            const int r_cy = bperm(carry, rq), r_ctr = bperm((int)ctr, rq), r_r = bperm(rr, rq), r_c = bperm(rc, rq);
-            const int r_tr = bperm(ctr_r, rq), r_tc = bperm(ctr_c, rq), r_dl = bperm(g_dl, rq);
-            const bool rht = r_cy != 0 && r_ctr != 0;
-            const bool waiting = p_tr == 0;
-            const int x1 = isr ? r_r : (waiting ? cell_r(p_sc) : 0);
-            const int x2 = isr ? r_c : (waiting ? cell_c(p_sc) : 0);
-            const int x3 = isr ? (rht ? r_tr : 0) : cell_r(p_tg);
-            const int x4 = isr ? (rht ? r_tc : 0) : cell_c(p_tg);
-            const int x5 = isr ? (rht ? r_dl : 0) : p_dl;
-            const bool hascar = !isr && !waiting && p_car != 0x7f;
-            const float d1 = qdiv_r(x1, yH), d2 = qdiv_r(x2, yW), d3 = qdiv_r(x3, yH), d4 = qdiv_r(x4, yW);
-            const float d5 = qdiv_r(x5, yT);
-            const float d6 = hascar ? qdiv_r(p_car, yM) : -1.0f;   // yM = 0 when MR <= 1
-            const float fl = isr ? (r_cy != 0 ? 1.0f : 0.0f) : (waiting ? 0.0f : 1.0f);
-            if (live) {
-                float* o = cv + (isr ? 6 * q : 6 * nr + 7 * (q - nr));
-                o[0] = d1;
-                o[1] = d2;
-                o[2] = isr ? fl : d3;
-                o[3] = isr ? d3 : d4;
-                o[4] = isr ? d4 : d5;
-                o[5] = isr ? d5 : fl;
-                if (!isr) o[6] = d6;
-            }
-        }
-    }
-}
-
-// The record pass alone (mdl_build_obs): env env_begin + w -> record row w.
-template <bool STALE>
-__global__ __launch_bounds__(256) void k_obs_small_rec(DevParams p, int env_begin, int n, ObsRec L,
-                                                       uint32_t* __restrict__ recs, int wpb, int lds_stride) {
+__global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, int n, float* __restrict__ amap,
+                                                   float* __restrict__ avec, float* __restrict__ cmap,
+                                                   float* __restrict__ cvec, int wpb, int lds_stride) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int wave = wave_id();
     const int lane = lane_id();
@@ -1024,6 +732,7 @@ __global__ __launch_bounds__(256) void k_obs_small_rec(DevParams p, int env_begi
     const int e = env_begin + w;
     const int A = p.A, P = p.P;
     const int mi = p.env_map ? p.env_map[e] : 0;
+    // ---- loads: robots, packages (+ tracker data), clock ----
     const uint32_t rv = lane < A ? p.rob[(size_t)e * A + lane] : 0u;
     uint64_t pkd = 0, tdd = 0;
     uint32_t f = 0;
@@ -1034,38 +743,7 @@ __global__ __launch_bounds__(256) void k_obs_small_rec(DevParams p, int env_begi
         if (STALE) tdd = p.trk[g];
     }
     const int t = p.es[e].t;
-    obs_small_record<STALE>(p, mi, rv, pkd, f, tdd, t, L, recs + (size_t)w * L.words, smem + (size_t)wave * lds_stride);
-}
-
-template <bool STALE>
-__global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, int n, float* __restrict__ amap,
-                                                   float* __restrict__ avec, float* __restrict__ cmap,
-                                                   float* __restrict__ cvec, int wpb, int lds_stride) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int wave = wave_id();
-    const int lane = lane_id();
-    if (wave >= wpb) return;
-    // a grid smaller than the batch: each wave takes envs w, w + (grid waves), ... -- its stores of
-    // one env drain while it computes the next
-    const int stride = (int)gridDim.x * wpb;
-    for (int w = xcd_block() * wpb + wave; w < n; w += stride) {
-        const int e = env_begin + w;
-        const int A = p.A, P = p.P;
-        const int mi = p.env_map ? p.env_map[e] : 0;
-        // ---- loads: robots, packages (+ tracker data), clock ----
-        const uint32_t rv = lane < A ? p.rob[(size_t)e * A + lane] : 0u;
-        uint64_t pkd = 0, tdd = 0;
-        uint32_t f = 0;
-        if (lane < P) {
-            const size_t g = (size_t)e * P + lane;
-            pkd = p.pkg[g];
-            f = p.pstate[g];
-            if (STALE) tdd = p.trk[g];
-        }
-        const int t = p.es[e].t;
-        wave_sync();   // the previous env's LDS reads are done before this one's writes
-        obs_small_emit<STALE>(p, w, mi, rv, pkd, f, tdd, t, amap, avec, cmap, cvec, smem + (size_t)wave * lds_stride);
-    }
+    obs_small_emit<STALE>(p, w, mi, rv, pkd, f, tdd, t, amap, avec, cmap, cvec, smem + (size_t)wave * lds_stride);
 }
 
 }  // namespace mdl

@@ -108,10 +108,10 @@ def test_small_builder_config3_vs_oracle():
                                   ("map4.txt", 3, 30, 40, 2, 5, 4, 7)],
                          ids=["7x7", "config3b", "19x20"])
 def test_flat_emission_any_alignment_and_range(case):
-    """The flat emission pass (csrc/mdl_obs_expand.hpp) writes every float of each tensor exactly
-    once, wherever the tensor starts inside a 16-B line (lead 0..3 floats), with float4s that
-    straddle envs / planes / agents (HW % 4 != 0, vector lengths % 4 != 0), and for an env
-    sub-range: bit-identical to the aligned full build, the sentinels around each tensor intact."""
+    """The builder writes every float of each tensor exactly once, wherever the tensor starts
+    inside a 16-B line (1..3 floats in: the unaligned emission paths), with float4s that straddle
+    envs / planes / agents (HW % 4 != 0, vector lengths % 4 != 0), and for an env sub-range:
+    bit-identical to the aligned full build, the sentinels around each tensor intact."""
     mg = _mg()
     m, A, P, T, MO, MP, MR, MPs = case
     g = grid(m)

@@ -234,3 +234,25 @@ def test_lib_path_override_needs_profiling_flag():
     env["PYTHONPATH"] = os.path.join(REPO, "marl-delivery_amd")
     r = subprocess.run([sys.executable, "-c", "import marl_gpu._lib"], env=env, capture_output=True, text=True)
     assert r.returncode != 0 and "MDL_PROFILING=1" in r.stderr, r.stderr[-500:]
+
+
+def test_traffic_json_recomputes_from_committed_profiles(tmp_path):
+    """bench.py's roofline.traffic comes from profiles/traffic.json; every record in it is recomputed
+    here from the per-dispatch PMC rows committed under profiles/ and the committed FETCH_SIZE
+    calibration (the measurement record is self-contained)."""
+    import json
+    tj = json.load(open(os.path.join(REPO, "profiles", "traffic.json")))
+    specs = []
+    for rec in tj["records"]:
+        src = rec["source"].split(" ", 1)[0]
+        assert src.startswith("profiles/") and os.path.isdir(os.path.join(REPO, src)), src
+        c = rec["config"]
+        specs.append(f"{rec['name']}={os.path.join(REPO, src)}:{c['envs']},{c['agents']},{c['packages']},"
+                     + "+".join(c["maps"]))
+    out = tmp_path / "traffic.json"
+    subprocess.check_call([sys.executable, os.path.join(REPO, "scripts", "traffic_json.py"), str(out),
+                           os.path.join(REPO, tj["calibration"])] + specs, stdout=subprocess.DEVNULL)
+    again = json.load(open(out))
+    for a, b in zip(tj["records"], again["records"]):
+        assert a["hbm_bytes_per_launch"] == b["hbm_bytes_per_launch"], a["name"]
+        assert a["fetch_dispatches"] == b["fetch_dispatches"] >= 100

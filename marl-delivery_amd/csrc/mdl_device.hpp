@@ -103,6 +103,10 @@ struct DevParams {
     int obs_plane_words;       // > 0: k_obs stages the map planes as bit words (LDS words reserved per wave)
     int obs_small;             // k_obs_small builds the observations (mdl_obs_small.hpp)
     int key7_dsh;              // > 0: (max(0,dl-t), rank, 7-bit order) fits 32 bits, dlc at this shift
+    // cost_fold[k] = the reference's k-fold move-cost sum for every k <= 64 robots (cost_sum's
+    // 9 entries, read in the step's first scalar batch, serve A <= 8; the wider kernels index
+    // this one instead of adding move_cost n_cost times in a dependent fp64 chain)
+    double cost_fold[65];
 };
 
 // Robot word: bits 0-15 cell (r | c<<8), bits 16-26 carried package id,

@@ -312,9 +312,10 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     p.delivery_reward = c.delivery_reward;
     p.delay_reward = c.delay_reward;
     {
-        double acc = 0.0;
-        for (int k = 0; k < 9; k++) {
-            p.cost_sum[k] = acc;
+        double acc = 0.0;   // ((0.0 + move_cost) + move_cost) ... k times: env.py:252-257's fold
+        for (int k = 0; k < 65; k++) {
+            if (k < 9) p.cost_sum[k] = acc;
+            p.cost_fold[k] = acc;
             acc += c.move_cost;
         }
     }

@@ -56,6 +56,9 @@
 #ifndef MDL_ABLATE
 #define MDL_ABLATE 0
 #endif
+#ifndef MDL_COST_FOLD_TAB
+#define MDL_COST_FOLD_TAB 1
+#endif
 
 namespace mdl {
 
@@ -361,6 +364,7 @@ struct StepArgs {
     int fmt, n, auto_reset, wpb, lds_stride, K;
 };
 typedef __attribute__((address_space(4))) const StepArgs* KargPtr;
+static_assert(sizeof(StepArgs) + 256 <= 4096, "the step's kernel arguments stay inside the 4 KiB kernarg segment");
 
 // The step kernel's leading arguments are preloaded into SGPRs by the command
 // processor (gfx950 kernarg preloading, -amdgpu-kernarg-preload-count=14 for this
@@ -787,6 +791,8 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
         double rr;
         if constexpr (AU > 0 && AU <= 8) {
             rr = p.cost_sum[n_cost];  // n_cost <= A <= 8: the same fold, tabulated on the host
+        } else if (MDL_COST_FOLD_TAB) {
+            rr = p.cost_fold[n_cost];  // n_cost <= A <= 64: likewise (one scalar load, no fp64 chain)
         } else {
             rr = 0.0;
             for (int k = 0; k < n_cost; k++) rr += p.move_cost;

@@ -118,6 +118,7 @@ struct MdlEngine {
     std::vector<void*> allocs;
     size_t lds_step = 0, lds_obs = 0;
     int wpb_step = 1, wpb_obs = 1;
+    int obs_rank_lds = 0;   // small builder: LDS bytes of the largest map's rank table (0: ranks read from L2)
     int n_cu = 0;   // compute units of the device (step_wpb)
     int maxHW = 0;
     bool seeded = false;
@@ -432,6 +433,17 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     eng->lds_obs = p.obs_small ? mdl::obs_lds_small((int)A, eng->maxHW, (int)P, p.MO, p.MP)
                                : mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MO, p.MP, p.MR, p.MPs);
     eng->wpb_obs = waves_per_block(eng->lds_obs);
+    // Worth it when the actor vectors take several tuple passes (each gathers ranks): config 3b
+    // (MO = MP = 100) 141-143 -> 135-137 us per build; with one pass (config 3) the block's table copy
+    // and barrier cost more than the two gathers they save (74.5 -> 76 us; profiles/r04/obs_rank_lds_ab.txt)
+    const int MPc_ = p.MP < (int)P ? p.MP : (int)P;
+    if (p.obs_small && MDL_OBS_RANK_LDS && (int)(A * A + A * MPc_ + A) > 64) {
+        for (int m = 0; m < n_maps; m++)
+            eng->obs_rank_lds = std::max(eng->obs_rank_lds, (int)(((2 * eng->mapH[m] - 1) * (2 * eng->mapW[m] - 1) * 2 + 15) & ~15));
+        // a workgroup's LDS: the table + wpb slices, within the per-CU budget of the builder's occupancy
+        if ((size_t)eng->obs_rank_lds + eng->lds_obs * eng->wpb_obs > LDS_BUDGET || eng->obs_rank_lds > 8192)
+            eng->obs_rank_lds = 0;
+    }
     if (const char* v = getenv("MDL_OBS_WPB")) {   // profiling override (1..4 waves per workgroup)
         const int x = atoi(v);
         if (x >= 1 && x < eng->wpb_obs) eng->wpb_obs = x;
@@ -529,7 +541,8 @@ int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, 
     }
     HIPCHK(mdl::launch_step(eng->p, actions, action_format, nullptr, E, auto_reset, r_env, r_shaped, done,
                             step_wpb(E, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, s));
-    HIPCHK(mdl::launch_obs(eng->p, 0, E, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs, eng->lds_obs, s));
+    HIPCHK(mdl::launch_obs(eng->p, 0, E, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs, eng->lds_obs, s,
+                           eng->obs_rank_lds));
     return 0;
 }
 
@@ -869,7 +882,7 @@ int mdl_build_obs(MdlEngine* eng, int32_t env_begin, int32_t n, float* actor_map
                     env_begin + n, eng->shape_run_end[env_begin]);
     DeviceGuard dg(eng->device);
     HIPCHK(mdl::launch_obs(eng->p, env_begin, n, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs,
-                           eng->lds_obs, (hipStream_t)stream));
+                           eng->lds_obs, (hipStream_t)stream, eng->obs_rank_lds));
     return 0;
 }
 

@@ -1945,14 +1945,20 @@ hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt
 }
 
 hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
-                      int wpb, size_t lds, hipStream_t s) {
+                      int wpb, size_t lds, hipStream_t s, int rank_lds) {
     if (p.obs_small) {
-        if (p.stale)
-            hipLaunchKernelGGL(k_obs_small<true>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin, n,
-                               amap, avec, cmap, cvec, wpb, (int)lds);
-        else
-            hipLaunchKernelGGL(k_obs_small<false>, dim3(blocks_for(n, wpb)), dim3(256), lds * wpb, s, p, env_begin,
-                               n, amap, avec, cmap, cvec, wpb, (int)lds);
+        const dim3 g(blocks_for(n, wpb)), b(256);
+        const size_t dyn = (size_t)rank_lds + lds * wpb;
+#define MDL_OBS_SMALL(ST, RL) \
+    hipLaunchKernelGGL((k_obs_small<ST, RL>), g, b, dyn, s, p, env_begin, n, amap, avec, cmap, cvec, wpb, (int)lds, rank_lds)
+        if (p.stale) {
+            if (rank_lds > 0) MDL_OBS_SMALL(true, true);
+            else MDL_OBS_SMALL(true, false);
+        } else {
+            if (rank_lds > 0) MDL_OBS_SMALL(false, true);
+            else MDL_OBS_SMALL(false, false);
+        }
+#undef MDL_OBS_SMALL
         return hipGetLastError();
     }
     if (p.stale)

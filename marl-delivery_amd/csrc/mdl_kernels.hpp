@@ -22,8 +22,13 @@ hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt
 hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
                            float* sh, uint8_t* done, float* amap, float* avec, float* cmap, float* cvec, int wpb,
                            size_t lds, hipStream_t s);
+#ifndef MDL_OBS_RANK_LDS
+#define MDL_OBS_RANK_LDS 1
+#endif
+// rank_lds > 0 (small builder): bytes of LDS in front of the per-wave slices holding the launch's
+// distance-rank table (mdl_obs_small.hpp k_obs_small)
 hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
-                      int wpb, size_t lds, hipStream_t s);
+                      int wpb, size_t lds, hipStream_t s, int rank_lds = 0);
 // A launch's own completion word (host-mapped): every wave of its grid counts itself in the
 // running device counter `ctr` (never reset: `base` is its value before the launch) after a
 // system-scope release of its stores; the last one writes `value` to `seq`.  seq == nullptr: none;

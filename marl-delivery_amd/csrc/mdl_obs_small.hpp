@@ -274,12 +274,14 @@ __host__ __device__ inline bool obs_small_ok(int A, int P, int key7_dsh, int max
 // them: lane a < A the robot word, lane j < P package j's table entry, state word and
 // (stale mode) tracker data, t the env clock.  k_obs_small loads them; the fused
 // step + observation kernel (k_step<..., OBS = true>) passes the step's registers.
-// `smem_wave` is this wave's LDS slice (obs_small_lds bytes).
+// `smem_wave` is this wave's LDS slice (obs_small_lds bytes).  rank_lds: the map's distance-rank
+// table already copied into the workgroup's LDS (k_obs_small), or null: read from global memory.
 template <bool STALE>
 __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi, uint32_t rv, uint64_t pkd,
                                                uint32_t f, uint64_t tdd, int t, float* __restrict__ amap,
                                                float* __restrict__ avec, float* __restrict__ cmap,
-                                               float* __restrict__ cvec, unsigned char* smem_wave) {
+                                               float* __restrict__ cvec, unsigned char* smem_wave,
+                                               const uint16_t* rank_lds = nullptr) {
     const int lane = lane_id();
     const int A = p.A, P = p.P;
     const MapDesc md = p.maps[mi];
@@ -289,7 +291,7 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
     const int MOc = MO < A - 1 ? MO : A - 1;
     const double yH = p.obs_recip[2 * mi], yW = p.obs_recip[2 * mi + 1];   // RN(1/H), RN(1/W)
     const double yT = p.obs_recip[2 * p.n_maps], yM = p.obs_recip[2 * p.n_maps + 1];
-    const uint16_t* rank = p.rank + md.rank_off;
+    const uint16_t* rank = rank_lds ? rank_lds : p.rank + md.rank_off;
     const int rW = 2 * W - 1, rOff = (H - 1) * rW + (W - 1);   // rank[(dr+H-1)*(2W-1) + dc+W-1]
 
     uint32_t* bits = (uint32_t*)smem_wave;                       // [5][NW] + guard, critic planes first
@@ -720,13 +722,24 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
     }
 }
 
-template <bool STALE>
+// rank_lds > 0: the launch's maps (one shape, so one rank table) have their table copied into the
+// first rank_lds bytes of the workgroup's LDS before the waves start: the package-order keys and the
+// other-robot order then gather ranks from LDS (~64 cycles) instead of L2 (hundreds)
+template <bool STALE, bool RL>
 __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, int n, float* __restrict__ amap,
                                                    float* __restrict__ avec, float* __restrict__ cmap,
-                                                   float* __restrict__ cvec, int wpb, int lds_stride) {
+                                                   float* __restrict__ cvec, int wpb, int lds_stride, int rank_lds) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int wave = wave_id();
     const int lane = lane_id();
+    uint16_t* rk = (uint16_t*)smem;
+    if constexpr (RL) {
+        const MapDesc md0 = p.maps[p.env_map ? p.env_map[env_begin] : 0];   // every env of the launch: one shape
+        const int nrk = (2 * md0.H - 1) * (2 * md0.W - 1);
+        const uint16_t* src = p.rank + md0.rank_off;
+        for (int i = (int)threadIdx.x; i < nrk; i += 256) rk[i] = src[i];
+        __syncthreads();   // every wave of the block is still here (none has returned yet)
+    }
     const int w = xcd_block() * wpb + wave;
     if (wave >= wpb || w >= n) return;
     const int e = env_begin + w;
@@ -743,7 +756,8 @@ __global__ __launch_bounds__(256) void k_obs_small(DevParams p, int env_begin, i
         if (STALE) tdd = p.trk[g];
     }
     const int t = p.es[e].t;
-    obs_small_emit<STALE>(p, w, mi, rv, pkd, f, tdd, t, amap, avec, cmap, cvec, smem + (size_t)wave * lds_stride);
+    obs_small_emit<STALE>(p, w, mi, rv, pkd, f, tdd, t, amap, avec, cmap, cvec,
+                          smem + rank_lds + (size_t)wave * lds_stride, RL ? rk : nullptr);
 }
 
 }  // namespace mdl

@@ -7,7 +7,7 @@
 //   map1   one record load per float4 (the shared planes' form)
 //   map2   two loads (bitset word + the agent's cell word, the one-hot planes' form)
 //   map3   the real plane mix: ch 0/3/4 one bitset word, ch 1/5 one agent word, ch 2 two words
-// against a plain fill of the same bytes and the wave-per-env slab shape.
+// against a plain fill of the same bytes and the wave-per-env slab shape (and 2 / 4 / 8 waves per env's slab, split or interleaved).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/expand_probe2.hip -o scripts/exp/expand_probe2.bin
 #include <hip/hip_runtime.h>
 
@@ -42,6 +42,27 @@ __global__ __launch_bounds__(256) void k_slab(f32x4* __restrict__ out, int n) {
     if (w >= n) return;
     f32x4* o = out + (size_t)w * PER4;
     for (int q = lane; q < PER4; q += 64) o[q] = f32x4{1.f, 0.f, 1.f, 0.f};
+}
+
+// S waves per env, wave s of env w writing the s-th of S equal parts of the env's slab
+template <int S>
+__global__ __launch_bounds__(256) void k_slabs(f32x4* __restrict__ out, int n) {
+    const int w2 = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int w = w2 / S, s = w2 % S;
+    if (w >= n) return;
+    f32x4* o = out + (size_t)w * PER4 + (size_t)s * (PER4 / S);
+    for (int q = lane; q < PER4 / S; q += 64) o[q] = f32x4{1.f, 0.f, 1.f, 0.f};
+}
+
+// S waves per env (S = 4: one workgroup), interleaved: the S waves write consecutive 1 KB pieces, so the
+// env's slab is written as one stream advancing S KB per round instead of S streams
+template <int S>
+__global__ __launch_bounds__(256) void k_slabs_il(f32x4* __restrict__ out, int n) {
+    const int w2 = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int w = w2 / S, s = w2 % S;
+    if (w >= n) return;
+    f32x4* o = out + (size_t)w * PER4;
+    for (int q = s * 64 + lane; q < PER4; q += 64 * S) o[q] = f32x4{1.f, 0.f, 1.f, 0.f};
 }
 
 template <int MODE>
@@ -115,6 +136,11 @@ int main() {
     for (int round = 0; round < 2; round++) {
         rep("fill", timeit([&] { hipLaunchKernelGGL(k_fill, dim3(nb), dim3(256), 0, 0, out, n4); }));
         rep("slab", timeit([&] { hipLaunchKernelGGL(k_slab, dim3(n / 4), dim3(256), 0, 0, out, n); }));
+        rep("slab_x2", timeit([&] { hipLaunchKernelGGL(k_slabs<2>, dim3(2 * n / 4), dim3(256), 0, 0, out, n); }));
+        rep("slab_x4", timeit([&] { hipLaunchKernelGGL(k_slabs<4>, dim3(4 * n / 4), dim3(256), 0, 0, out, n); }));
+        rep("slab_x8", timeit([&] { hipLaunchKernelGGL(k_slabs<8>, dim3(8 * n / 4), dim3(256), 0, 0, out, n); }));
+        rep("slab_il2", timeit([&] { hipLaunchKernelGGL(k_slabs_il<2>, dim3(2 * n / 4), dim3(256), 0, 0, out, n); }));
+        rep("slab_il4", timeit([&] { hipLaunchKernelGGL(k_slabs_il<4>, dim3(4 * n / 4), dim3(256), 0, 0, out, n); }));
         rep("map1", timeit([&] { hipLaunchKernelGGL(k_map<1>, dim3(nb), dim3(256), 0, 0, out, n4, rec); }));
         rep("map2", timeit([&] { hipLaunchKernelGGL(k_map<2>, dim3(nb), dim3(256), 0, 0, out, n4, rec); }));
         rep("map3", timeit([&] { hipLaunchKernelGGL(k_map<3>, dim3(nb), dim3(256), 0, 0, out, n4, rec); }));

@@ -7,7 +7,7 @@
 //   map1   one record load per float4 (the shared planes' form)
 //   map2   two loads (bitset word + the agent's cell word, the one-hot planes' form)
 //   map3   the real plane mix: ch 0/3/4 one bitset word, ch 1/5 one agent word, ch 2 two words
-// against a plain fill of the same bytes and the wave-per-env slab shape (and 2 / 4 / 8 waves per env's slab, split or interleaved).
+// against a plain fill of the same bytes and the wave-per-env slab shape (and 2 / 4 / 8 / 64 / 256 waves per env's slab, split or interleaved; persistent waves).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/expand_probe2.hip -o scripts/exp/expand_probe2.bin
 #include <hip/hip_runtime.h>
 
@@ -63,6 +63,15 @@ __global__ __launch_bounds__(256) void k_slabs_il(f32x4* __restrict__ out, int n
     if (w >= n) return;
     f32x4* o = out + (size_t)w * PER4;
     for (int q = s * 64 + lane; q < PER4; q += 64 * S) o[q] = f32x4{1.f, 0.f, 1.f, 0.f};
+}
+
+// persistent: NWV waves in all, wave v writing the slabs of envs v, v + NWV, ... one after another
+__global__ __launch_bounds__(256) void k_slab_persist(f32x4* __restrict__ out, int n, int nwv) {
+    const int v = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (int w = v; w < n; w += nwv) {
+        f32x4* o = out + (size_t)w * PER4;
+        for (int q = lane; q < PER4; q += 64) o[q] = f32x4{1.f, 0.f, 1.f, 0.f};
+    }
 }
 
 template <int MODE>
@@ -141,6 +150,10 @@ int main() {
         rep("slab_x8", timeit([&] { hipLaunchKernelGGL(k_slabs<8>, dim3(8 * n / 4), dim3(256), 0, 0, out, n); }));
         rep("slab_il2", timeit([&] { hipLaunchKernelGGL(k_slabs_il<2>, dim3(2 * n / 4), dim3(256), 0, 0, out, n); }));
         rep("slab_il4", timeit([&] { hipLaunchKernelGGL(k_slabs_il<4>, dim3(4 * n / 4), dim3(256), 0, 0, out, n); }));
+        rep("slab_x64", timeit([&] { hipLaunchKernelGGL(k_slabs<64>, dim3(64 * n / 4), dim3(256), 0, 0, out, n); }));
+        rep("slab_x256", timeit([&] { hipLaunchKernelGGL(k_slabs<256>, dim3(256 * n / 4), dim3(256), 0, 0, out, n); }));
+        rep("persist1024", timeit([&] { hipLaunchKernelGGL(k_slab_persist, dim3(256), dim3(256), 0, 0, out, n, 1024); }));
+        rep("persist2048", timeit([&] { hipLaunchKernelGGL(k_slab_persist, dim3(512), dim3(256), 0, 0, out, n, 2048); }));
         rep("map1", timeit([&] { hipLaunchKernelGGL(k_map<1>, dim3(nb), dim3(256), 0, 0, out, n4, rec); }));
         rep("map2", timeit([&] { hipLaunchKernelGGL(k_map<2>, dim3(nb), dim3(256), 0, 0, out, n4, rec); }));
         rep("map3", timeit([&] { hipLaunchKernelGGL(k_map<3>, dim3(nb), dim3(256), 0, 0, out, n4, rec); }));

@@ -442,11 +442,47 @@ __device__ __forceinline__ float cvt_ub(uint32_t y) {
     return f;
 }
 
+// One plane of emit_maps_bitrows, its kind fixed at compile time (0 a bit row as is, 1 a one-hot
+// of cell `own`, 2 the bit row less `own` plus the multi-robot row), the float4 loop unrolled by
+// BITROWS_U: the unrolled group's LDS words are all read before the first is used and its stores
+// issue back to back (one kind branch per plane instead of per float4, one LDS wait per group).
+#ifndef MDL_BITROWS_U
+#define MDL_BITROWS_U 4
+#endif
+template <int KIND>
+__device__ __forceinline__ void bitrow_plane(GLOBAL char* base, const uint32_t* row, const uint32_t* mrow, int own,
+                                             int qpp, int lane, uint32_t sh) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    constexpr int U = MDL_BITROWS_U;
+    auto put = [&](int q, uint32_t b) {
+        const uint32_t y = (b * 0x204081u) & 0x01010101u;   // bit i -> byte i (b < 16: no carries)
+        *(GLOBAL f32x4*)(base + ((uint32_t)q << 4)) = f32x4{cvt_ub<0>(y), cvt_ub<1>(y), cvt_ub<2>(y), cvt_ub<3>(y)};
+    };
+    auto bits = [&](int q, uint32_t r, uint32_t m) -> uint32_t {
+        if constexpr (KIND == 1) return onehot4(own, q << 2);
+        else if constexpr (KIND == 2) return (__builtin_amdgcn_ubfe(r, sh, 4u) & ~onehot4(own, q << 2)) |
+                                             __builtin_amdgcn_ubfe(m, sh, 4u);
+        else return __builtin_amdgcn_ubfe(r, sh, 4u);
+    };
+    int q = lane, k = 0;
+    for (; q + (U - 1) * WAVE < qpp; q += U * WAVE, k += 8 * U) {   // uniform (qpp % 64 == 0 for the maps here)
+        uint32_t r[U], m[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            r[u] = KIND != 1 ? row[k + 8 * u] : 0u;
+            m[u] = KIND == 2 ? mrow[k + 8 * u] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) put(q + u * WAVE, bits(q + u * WAVE, r[u], m[u]));
+    }
+    for (; q < qpp; q += WAVE, k += 8)
+        put(q, bits(q, KIND != 1 ? row[k] : 0u, KIND == 2 ? mrow[k] : 0u));
+}
+
 __device__ inline void emit_maps_bitrows(const FeatLds& L, int NW, int HW, int A, float* am, float* cm) {
     const int lane = lane_id();
     const int qpp = HW >> 2;
     const uint32_t sh = (uint32_t)(lane & 7) << 2;
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
     const int np = 6 * A + 4;
     for (int pl = 0; pl < np; pl++) {   // uniform
         const bool actor = pl < 6 * A;
@@ -457,24 +493,12 @@ __device__ inline void emit_maps_bitrows(const FeatLds& L, int NW, int HW, int A
         const int kind = actor ? (ch == 1 ? 1 : ch == 2 ? 2 : ch == 5 ? 5 : 0) : 0;
         const int set = actor ? (ch == 0 ? BS_GRID : ch == 2 ? BS_ROBOT : ch == 3 ? BS_WSTART : BS_ATARGET)
                               : (ch == 0 ? BS_GRID : ch == 1 ? BS_ROBOT : ch == 2 ? BS_WSTART : BS_ATARGET);
-        const int own = L.rcell[a], tgt = L.rtgt[a];
         const uint32_t* row = L.bits + set * NW + (lane >> 3);
         const uint32_t* mrow = L.bits + BS_MULTI * NW + (lane >> 3);
         GLOBAL char* base = (GLOBAL char*)dst;
-        for (int q = lane, k = 0; q < qpp; q += WAVE, k += 8) {
-            const int c0 = q << 2;
-            uint32_t b;
-            if (kind == 1) {
-                b = onehot4(own, c0);
-            } else if (kind == 5) {
-                b = onehot4(tgt, c0);
-            } else {
-                b = __builtin_amdgcn_ubfe(row[k], sh, 4u);
-                if (kind == 2) b = (b & ~onehot4(own, c0)) | __builtin_amdgcn_ubfe(mrow[k], sh, 4u);
-            }
-            const uint32_t y = (b * 0x204081u) & 0x01010101u;   // bit i -> byte i (b < 16: no carries)
-            *(GLOBAL f32x4*)(base + ((uint32_t)q << 4)) = f32x4{cvt_ub<0>(y), cvt_ub<1>(y), cvt_ub<2>(y), cvt_ub<3>(y)};
-        }
+        if (kind == 0) bitrow_plane<0>(base, row, mrow, 0, qpp, lane, sh);
+        else if (kind == 2) bitrow_plane<2>(base, row, mrow, L.rcell[a], qpp, lane, sh);
+        else bitrow_plane<1>(base, row, mrow, kind == 1 ? L.rcell[a] : L.rtgt[a], qpp, lane, sh);
     }
 }
 

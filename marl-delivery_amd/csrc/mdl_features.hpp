@@ -580,9 +580,15 @@ __host__ __device__ inline int actor_compact_dim(int A, int MO, int MPc) {
 __host__ __device__ inline int critic_compact_dim(int A, int MR, int MPsc) {
     return 6 * (A < MR ? A : MR) + 7 * MPsc + 1;
 }
-// agents whose compact actor rows are staged together (<= 2048 floats, >= 1 agent)
+// agents whose compact actor rows are staged together (<= MDL_STAGE_FLOATS floats, >= 1 agent).
+// The staging slice is most of the general builder's LDS per wave (config 5: 16 agents x 182 floats),
+// and that LDS sets its occupancy: 512 floats (2 agents there) leave the critic row as the largest
+// staged item (797 floats) and take the slice from 17.1 to 12.3 KB per wave.
+#ifndef MDL_STAGE_FLOATS
+#define MDL_STAGE_FLOATS 512
+#endif
 __host__ __device__ inline int actor_group(int na, int Dc) {
-    const int g = 2048 / Dc;
+    const int g = MDL_STAGE_FLOATS / Dc;
     return g < 1 ? 1 : (g < na ? g : na);
 }
 

@@ -13,11 +13,21 @@ replayed from hipGraphs of G steps each (launch-bound loop; the same kernels
 as eager launches).  value = agent-steps/s over all ranks (weak scaling: 4096
 envs per GPU, no collective on the step path; ``--total-envs N`` splits N envs
 over the ranks instead: strong scaling, SURVEY.md 8(e), global env ids and seeds
-unchanged).
+unchanged).  ``--config 3`` times the trainer's per-step cost instead: one
+``mdl_step_obs`` (step + the full 6ch/4ch maps and vectors of the new state) over
+16,384 envs per GPU.
 
-Extra fields: eager (un-captured) throughput, the roofline record of the step
-kernel (HIP-event timed), and the CPU baseline (the oracle's C restatement,
-single thread, on a bounded sample of the same workload).
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the
+process is one rank.  A plain ``python bench.py --gpus N`` (N > 1, no WORLD_SIZE)
+starts ``python -m torch.distributed.run --nproc-per-node N bench.py ...`` as a
+child process -- the parent makes no GPU call -- forwards rank 0's JSON line and
+exits with the child's return code.
+
+Extra fields: the ranks the process group saw and their devices, eager
+(un-captured) throughput, the launch floor (an empty kernel in the step's launch
+shape replayed the same way), the roofline record of the step kernel (HIP-event
+timed), and the CPU baseline (the oracle's C restatement on a bounded sample of
+the same workload, timed on rank 0 after the timed region).
 """
 from __future__ import annotations
 
@@ -25,6 +35,7 @@ import argparse
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
@@ -38,31 +49,40 @@ import torch  # noqa: E402
 STEP_BYTES_PER_ENV = lambda A, P: 9 * A + 10 * P + 41  # SURVEY.md §8(d) / A.7  # noqa: E731
 HBM_PEAK_GBS = 8000.0                                     # MI355X_MICROARCH.md: 8.0 TB/s spec
 
+# config 3's observation dims (MAPPO/trainer.py:250-280: generate_vector_features(..., A-1, 5),
+# convert_global_state with the defaults MR = MPs = 100)
+OBS3 = dict(max_other_robots=4, max_packages_obs=5, max_robots_state=100, max_packages_state=100)
+OBS5 = dict(max_other_robots=15, max_packages_obs=20, max_robots_state=16, max_packages_state=100)
 
 # BASELINE.json configs run by --config (configs[1] is the headline; 4 and 5 are the
 # fixed-size multi-GPU batches, split over the ranks: strong scaling of one global batch)
 CONFIGS = {
-    "2": dict(maps=["map1.txt"], agents=5, packages=50, T=500, total=0,
+    "2": dict(maps=["map1.txt"], agents=5, packages=50, T=500, total=0, envs=4096,
               metric="agent-steps/sec (whole node), map1 5-agent 4096 envs, 1/2/4/8 MI355X"),
-    "4": dict(maps=[f"map{i}.txt" for i in range(1, 6)], agents=5, packages=50, T=500, total=65536,
+    "3": dict(maps=["map1.txt"], agents=5, packages=50, T=500, total=0, envs=16384,
+              metric="agent-steps/sec (whole node), map1 5-agent 16384 envs per GPU, step + full 6ch/4ch "
+                     "spatial + vector observations, 1/2/4/8 MI355X"),
+    "4": dict(maps=[f"map{i}.txt" for i in range(1, 6)], agents=5, packages=50, T=500, total=65536, envs=4096,
               metric="agent-steps/sec (whole node), map1-map5 mixed 5-agent 65536 envs, 1/2/4/8 MI355X"),
-    "5": dict(maps=["synthetic64.txt"], agents=16, packages=100, T=500, total=131072,
+    "5": dict(maps=["synthetic64.txt"], agents=16, packages=100, T=500, total=131072, envs=4096,
               metric="agent-steps/sec (whole node), synthetic 64x64 16-agent 131072 envs, 1/2/4/8 MI355X"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1, help="ranks of the job: must equal WORLD_SIZE (1 without torchrun)")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (= ranks, one process each); N > 1 without torch.distributed.run starts it as a child")
     ap.add_argument("--config", default="2", choices=sorted(CONFIGS),
-                    help="BASELINE.json config: 2 = map1 4096 envs per GPU (the headline), 4 = 65536 mixed-map "
-                         "envs over all ranks, 5 = 131072 synthetic 64x64 16-agent envs over all ranks")
+                    help="BASELINE.json config: 2 = map1 4096 envs per GPU (the headline), 3 = map1 16384 envs per "
+                         "GPU with full observations every step, 4 = 65536 mixed-map envs over all ranks, "
+                         "5 = 131072 synthetic 64x64 16-agent envs over all ranks")
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: 4096; config 3: 16384)")
     ap.add_argument("--total-envs", type=int, default=0,
                     help="strong scaling: this many envs in total, split over the ranks (0 = weak: --envs per GPU)")
-    ap.add_argument("--map", default=None, help="config 2 only (default map1.txt)")
+    ap.add_argument("--map", default=None, help="configs 2 / 3 only (default map1.txt)")
     ap.add_argument("--agents", type=int, default=None)
     ap.add_argument("--packages", type=int, default=None)
     ap.add_argument("--T", type=int, default=None)
@@ -71,56 +91,67 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget per leg (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--fused-k", type=int, default=100, help="bench mode (ii): steps per fused launch (0 = skip)")
+    ap.add_argument("--no-floor", action="store_true", help="skip the launch-floor leg")
     ap.add_argument("--no-graph", action="store_true", help="eager launches only (PMC profiling passes)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend under torchrun (gloo: rehearse N ranks on fewer GPUs)")
     ap.add_argument("--host-wait", default="auto", choices=("auto", "spin", "yield", "blocking"),
                     help="how the host waits for the GPU in synchronize (hipSetDeviceFlags schedule mode)")
     ap.add_argument("--graph-only", action="store_true",
-                    help="skip the eager and isolated-launch legs (rocprof kernel-trace pass: the trace then holds "
-                         "only the warmup and the timed graph replay, so its average is the timed region's)")
-    a = ap.parse_args()
+                    help="skip the eager, isolated-launch and floor legs (rocprof kernel-trace pass: the trace then "
+                         "holds only the warmup and the timed graph replay, so its average is the timed region's)")
+    a = ap.parse_args(argv)
     c = CONFIGS[a.config]
-    if a.map is not None and a.config != "2":
-        ap.error("--map applies to config 2 only")
+    if a.map is not None and a.config not in ("2", "3"):
+        ap.error("--map applies to configs 2 and 3 only")
     a.maps = [a.map] if a.map is not None else c["maps"]
     a.agents = c["agents"] if a.agents is None else a.agents
     a.packages = c["packages"] if a.packages is None else a.packages
     a.T = c["T"] if a.T is None else a.T
+    a.envs = c["envs"] if a.envs is None else a.envs
     if c["total"] and a.total_envs == 0:
         a.total_envs = c["total"]
     a.metric = c["metric"]
     return a
 
 
-def cpu_baseline(args, grid, seeds0, budget_s, n_threads, E, map_name):
-    """The oracle's C restatement on the same workload: the first rank's first
-    same-map run of E envs, same seeds, uniform trainer-int actions, for as many
-    steps as fit in ~budget_s of wall time, on `n_threads` OpenMP threads (envs
-    split statically across threads, SURVEY.md §8(d) CPU leg (ii))."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as O
-    A = args.agents
-    ob = O.OracleBatch(E, grid, A, args.packages, args.T, seed_base=int(seeds0), clear_on_reset=False)
-    gen = torch.Generator().manual_seed(0)
-    t_all = 0.0
-    steps = 0
-    while t_all < budget_s:
-        ints = torch.randint(0, 15, (E, A), generator=gen, dtype=torch.uint8).numpy()
-        t0 = time.perf_counter()
-        ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS, n_threads=n_threads)
-        t_all += time.perf_counter() - t0
-        steps += 1
-    host = host_cpu_info()
-    how = "single thread" if n_threads == 1 else f"{n_threads} OpenMP threads"
-    return {"value": E * A * steps / t_all, "unit": "agent-steps/s", "cores": n_threads, "kind": "port",
-            "sample": f"{E} envs ({map_name}) x {steps} steps ({E * A * steps} agent-steps, {t_all:.1f} s) of the "
-                      f"same workload, oracle/mdl_oracle.c, {how}, host {host['lscpu_model_name']}",
-            "host": host,
-            "threads_note": f"threads = min(affinity {host['affinity_cpus']}, cap {host['thread_cap']}): the cap is "
-                            f"a one-GPU box's CPU share; nproc {host['nproc']} counts the whole machine"}
+# ---------------------------------------------------------------- self-launch (N > 1, plain command)
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
+def launcher_cmd(n, argv, port):
+    """The torch.distributed.run command that runs this bench as n ranks (one per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def forward_child(cmd, env=None):
+    """Run `cmd`; its JSON result line goes to our stdout, every other line to stderr (progress
+    stays visible while it runs).  Returns the child's exit code."""
+    p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            sys.stdout.write(s + "\n")
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
+def self_launch(args, argv):
+    """`python bench.py --gpus N` (N > 1) outside torchrun: N ranks as a child torchrun job.
+    Nothing here touches the GPU (the children select and initialise their own devices)."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
+    env["MDL_BENCH_LAUNCHER"] = "self"
+    return forward_child(launcher_cmd(args.gpus, argv, free_port()), env)
+
+
+# ---------------------------------------------------------------- CPU baseline
 CPU_THREAD_CAP = 16   # a one-GPU box's CPU share (the pool's limit: nproc shows the whole machine)
 
 
@@ -155,9 +186,39 @@ def host_cpu_info():
             "threads_used": max(1, min(CPU_THREAD_CAP, aff))}
 
 
-def cpu_threads():
-    """This process's CPU share: the affinity mask, capped at CPU_THREAD_CAP (reported beside it)."""
-    return host_cpu_info()["threads_used"]
+def cpu_baseline(args, grid, seeds0, budget_s, n_threads, E, map_name, host, with_obs=False):
+    """The oracle's C restatement on the same workload: the first rank's first same-map run of
+    E envs, same seeds, uniform trainer-int actions, for as many steps as fit in ~budget_s of
+    wall time, on `n_threads` OpenMP threads (envs split statically across threads, SURVEY.md
+    §8(d) CPU leg (ii)).  with_obs (config 3): every step also builds the full observations
+    of the new state (MAPPO/trainer.py:261-280)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    A = args.agents
+    ob = O.OracleBatch(E, grid, A, args.packages, args.T, seed_base=int(seeds0), clear_on_reset=False)
+    obs_out = None
+    gen = torch.Generator().manual_seed(0)
+    t_all = 0.0
+    steps = 0
+    while t_all < budget_s:
+        ints = torch.randint(0, 15, (E, A), generator=gen, dtype=torch.uint8).numpy()
+        t0 = time.perf_counter()
+        ob.step(ints, auto_reset=True, consts=O.MAPPO_CONSTS, n_threads=n_threads)
+        if with_obs:
+            obs_out = ob.obs(args.T, OBS3["max_other_robots"], OBS3["max_packages_obs"], OBS3["max_robots_state"],
+                             OBS3["max_packages_state"], out=obs_out, n_threads=n_threads)
+        t_all += time.perf_counter() - t0
+        steps += 1
+    how = "single thread" if n_threads == 1 else f"{n_threads} OpenMP threads"
+    what = "step + full observations" if with_obs else "step"
+    rec = {"value": E * A * steps / t_all, "unit": "agent-steps/s", "cores": n_threads, "kind": "port",
+           "sample": f"{E} envs ({map_name}) x {steps} steps ({E * A * steps} agent-steps, {t_all:.1f} s) of the "
+                     f"same workload ({what}), oracle/mdl_oracle.c, {how}, host {host['lscpu_model_name']}",
+           "host": host}
+    rec["threads_note"] = ("single thread (one core of the host)" if n_threads == 1 else
+                           f"threads = min(affinity {host['affinity_cpus']}, cap {host['thread_cap']}): the cap is a "
+                           f"one-GPU box's CPU share; nproc {host['nproc']} counts the whole machine")
+    return rec
 
 
 HIP_SCHEDULE = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}   # hipDeviceSchedule* flags
@@ -174,14 +235,24 @@ def set_host_wait(mode):
     return int(hip.hipSetDeviceFlags(ctypes.c_uint(HIP_SCHEDULE[mode])))
 
 
-def main():
-    args = parse()
+def device_record(rank, local, dev_index):
+    pr = torch.cuda.get_device_properties(dev_index)
+    bus = "%04x:%02x:%02x" % (getattr(pr, "pci_domain_id", 0), getattr(pr, "pci_bus_id", 0),
+                              getattr(pr, "pci_device_id", 0))
+    return {"rank": rank, "local_rank": local, "device": dev_index, "pci": bus, "name": pr.name,
+            "arch": getattr(pr, "gcnArchName", "")}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args, argv)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world:   # one process per GPU: N GPUs need N ranks (torch.distributed.run)
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; run N > 1 as "
-                         f"python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}")
+    if args.gpus != world:   # one process per GPU: N GPUs need N ranks
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:   # under torchrun: always a process group
         import torch.distributed as dist
@@ -195,6 +266,13 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     host_wait_rc = set_host_wait(args.host_wait)
+    ranks_seen = dist.get_world_size() if dist is not None else 1
+    me = device_record(rank, local, dev.index)
+    if dist is not None:
+        devices = [None] * ranks_seen
+        dist.all_gather_object(devices, me)
+    else:
+        devices = [me]
 
     import marl_gpu
     from marl_gpu.maps import grid_array, load_map, map_path
@@ -214,8 +292,8 @@ def main():
     E = len(ids)
     if E == 0:
         raise SystemExit(f"bench.py: rank {rank} has no envs (--total-envs {args.total_envs} < {world} ranks)")
-    obs_dims = dict(max_other_robots=15, max_packages_obs=20, max_robots_state=16, max_packages_state=100) \
-        if args.config == "5" else dict(max_packages_obs=5)
+    obs_cfg = args.config == "3"
+    obs_dims = OBS5 if args.config == "5" else OBS3
     env = marl_gpu.BatchedEnv(grids if len(grids) > 1 else grids[0], E, A, P, args.T, seeds=seeds, env_map=env_map,
                               tracker="mappo", shaping="mappo", device=dev, **obs_dims)
     env.reset()
@@ -228,44 +306,14 @@ def main():
     r = torch.zeros(E, dtype=torch.float64, device=dev)
     sh = torch.zeros(E, dtype=torch.float32, device=dev)
     dn = torch.zeros(E, dtype=torch.uint8, device=dev)
+    obs_bufs = env.obs_buffers(E) if obs_cfg else None
 
-    def one(k):
-        env.step(acts[k % G], auto_reset=True, out=(r, sh, dn))
-
-    # capture G steps in a hipGraph (torch's stream capture covers the ctypes launches);
-    # done before the warmup, so that the warmup steps run right before the timed region
-    # (the capture keeps the GPU idle for milliseconds)
-    graph = None
-    if not args.no_graph:
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream())
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(s):
-            one(0)  # prime on the side stream
-            torch.cuda.synchronize()
-            with torch.cuda.graph(graph, stream=s):
-                for k in range(G):
-                    one(k)
-        torch.cuda.synchronize()
-        # one untimed replay: the first launch of a fresh graph uploads it (kernel-argument
-        # buffers, packet templates) and must not land inside the timed region
-        graph.replay()
-        torch.cuda.synchronize()
-
-    # warmup: W steps of the same kernel, launched the way the timed steps are (one replay of a
-    # W-step graph; eager launches without graphs)
-    if graph is not None and args.warmup > 0:
-        wg = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(wg, stream=s):
-                for k in range(args.warmup):
-                    one(k)
-        torch.cuda.synchronize()
-        wg.replay()
+    if obs_cfg:
+        def one(k):   # the trainer's per-step cost: step + the observations of the new state
+            env.step_obs(acts[k % G], auto_reset=True, out=(r, sh, dn), obs_out=obs_bufs)
     else:
-        for k in range(args.warmup):
-            one(k)
-    torch.cuda.synchronize()
+        def one(k):
+            env.step(acts[k % G], auto_reset=True, out=(r, sh, dn))
 
     def barrier():
         if dist is not None:
@@ -282,22 +330,62 @@ def main():
             dist.barrier()
         return dt
 
-    # ---- timed region: K steps replayed from graphs ----
-    barrier()
-    # the opening HIP event is enqueued on the idle stream before the clock starts: it marks the
-    # GPU-side start of the region (kernel_us below) and is not part of the K steps' work
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    t0 = time.perf_counter()
-    if graph is not None:
+    side = torch.cuda.Stream(device=dev)
+
+    def graph_region(fn):
+        """K calls of fn(k): captured as a G-call hipGraph (torch's stream capture covers the
+        ctypes launches), replayed once untimed (the first launch of a fresh graph uploads it),
+        then W warmup calls as one replay of a W-call graph (launched the way the timed calls
+        are, right before the timed region), then barrier + the timed n_graph replays.
+        Returns (max-over-ranks is applied by the caller) wall seconds and HIP-event ms."""
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            fn(0)  # prime on the side stream
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=side):
+                for k in range(G):
+                    fn(k)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        if args.warmup > 0:
+            wg = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(wg, stream=side):
+                    for k in range(args.warmup):
+                        fn(k)
+            torch.cuda.synchronize()
+            wg.replay()
+            torch.cuda.synchronize()
+            del wg
+        barrier()
+        # the opening HIP event is enqueued on the idle stream before the clock starts: it marks the
+        # GPU-side start of the region and is not part of the K steps' work
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        t0 = time.perf_counter()
         for _ in range(n_graph):
-            graph.replay()
+            g.replay()
+        e1.record()
+        w = stop_clock(t0)
+        return w, e0.elapsed_time(e1)
+
+    # ---- timed region: K steps replayed from graphs ----
+    if not args.no_graph:
+        wall, gpu_ms = graph_region(one)
     else:
+        for k in range(args.warmup):
+            one(k)
+        barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        t0 = time.perf_counter()
         for k in range(K):
             one(k)
-    ev1.record()
-    wall = stop_clock(t0)
-    gpu_ms = ev0.elapsed_time(ev1)
+        ev1.record()
+        wall = stop_clock(t0)
+        gpu_ms = ev0.elapsed_time(ev1)
 
     # ---- eager throughput (same kernels, one ctypes launch per step) ----
     wall_eager = None
@@ -308,9 +396,15 @@ def main():
             one(k)
         wall_eager = stop_clock(t1)
 
+    # ---- launch floor: an empty kernel in mdl_step's launch shape (grid, workgroup, LDS,
+    # kernel-argument layout), replayed exactly as the timed steps are ----
+    wall_floor = gpu_ms_floor = None
+    if not obs_cfg and not args.no_graph and not args.graph_only and not args.no_floor:
+        wall_floor, gpu_ms_floor = graph_region(lambda k: env.step_floor())
+
     # ---- bench mode: fused_k steps per launch, each env's
     # state in registers between steps; same action stream; not the API path ----
-    wall_f, nf, Kf = None, 0, args.fused_k
+    wall_f, nf, Kf = None, 0, (0 if obs_cfg else args.fused_k)
     if Kf > 0:
         facts = acts.repeat((Kf + G - 1) // G, 1, 1)[:Kf].contiguous()
         fr = torch.empty((Kf, E), dtype=torch.float64, device=dev)
@@ -342,17 +436,25 @@ def main():
         kdur_iso_us = float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]) * 1e3)
 
     if dist is not None:
-        t = torch.tensor([wall, wall_eager or 0.0, wall_f or 0.0], dtype=torch.float64,
+        t = torch.tensor([wall, wall_eager or 0.0, wall_f or 0.0, wall_floor or 0.0], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t[0])
         wall_eager = float(t[1]) if wall_eager is not None else None
         wall_f = float(t[2]) if wall_f is not None else None
+        wall_floor = float(t[3]) if wall_floor is not None else None
 
     total_agent_steps = E_all * A * K
     value = total_agent_steps / wall
     if rank == 0:
-        per_launch_bytes = STEP_BYTES_PER_ENV(A, P) * E
+        H0, W0 = grids[runs[0][0]].shape
+        obs_bytes_env = 4 * (A * 6 * H0 * W0 + A * env.actor_vec_dim + 4 * H0 * W0 + env.critic_vec_dim)
+        # algorithmic bytes per launch: the step's SoA traffic; config 3 adds the
+        # observation bytes it writes (the fused launch builds them from the step's registers, so
+        # the 474 B per env of state that SURVEY §8(d) counts for a separate builder's reload are
+        # not moved and not counted)
+        per_env = STEP_BYTES_PER_ENV(A, P) + (obs_bytes_env if obs_cfg else 0)
+        per_launch_bytes = per_env * E
         achieved = per_launch_bytes / (kdur_us * 1e-6) / 1e9
         traffic, traffic_rec = None, None
         if os.path.exists(args.traffic_json):
@@ -360,53 +462,77 @@ def main():
                 tj = json.load(open(args.traffic_json))
                 want = {"envs": E, "agents": A, "packages": P, "maps": args.maps}
                 for rec in tj.get("records", []):
-                    if rec.get("config") == want:
+                    if rec.get("config") == want and bool(rec.get("obs")) == obs_cfg:
                         traffic, traffic_rec = rec.get("hbm_bytes_per_launch"), rec
             except (OSError, ValueError):
                 traffic = None
         cpu = cpu1 = None
-        if world == 1 and args.cpu_seconds > 0:
-            nt = cpu_threads()
+        if args.cpu_seconds > 0:   # after every rank's timed region (the others wait in the closing barrier)
+            host = host_cpu_info()
+            nt = host["threads_used"]
             m0, b0, n0 = runs[0]
             Ec = min(n0, 4096)   # the first same-map run, at most 4096 envs (a bounded sample)
-            cpu = cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, nt, Ec, args.maps[m0])
-            cpu1 = cpu if nt == 1 else cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, 1, Ec, args.maps[m0])
-        kname = {"2": "mdl::k_step<true, 1, false, 5>", "4": "mdl::k_step<true, 1, false, 5> (mixed maps)",
-                 "5": "mdl::k_step<true, 2, false, 16>"}[args.config] if (A, P) == (CONFIGS[args.config]["agents"],
-                                                                              CONFIGS[args.config]["packages"]) \
-            else "mdl::k_step"
+            cpu = cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, nt, Ec, args.maps[m0], host, obs_cfg)
+            cpu1 = cpu if nt == 1 else cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, 1, Ec,
+                                                     args.maps[m0], host, obs_cfg)
+        std = (A, P) == (CONFIGS[args.config]["agents"], CONFIGS[args.config]["packages"])
+        kname = {"2": "mdl::k_step<true, 1, false, 5>", "3": "mdl::k_step_obs<true, 5>",
+                 "4": "mdl::k_step<true, 1, false, 5> (mixed maps)",
+                 "5": "mdl::k_step<true, 2, false, 16>"}[args.config] if std else "mdl::k_step"
+        ms_step = wall / K * 1e3
+        floor = None
+        if wall_floor is not None:
+            floor = {"kernel": "mdl::k_step_floor (empty; mdl_step's grid, workgroup size, LDS request and "
+                               "kernel-argument layout)",
+                     "ms_per_step": wall_floor / K * 1e3, "gpu_event_us_per_step": gpu_ms_floor / K * 1e3,
+                     "note": "replayed like the timed steps (G-node graphs, same warmup, same K); over_floor_us = "
+                             "the step's wall time per step minus this floor's: the step kernel's own cost"}
+        what = ("mdl_step_obs (step + MAPPO shaped reward + tracker + auto-reset, then the 6ch actor maps, "
+                f"{env.actor_vec_dim}-dim actor vectors, 4ch critic map and {env.critic_vec_dim}-dim critic vector "
+                "of the new state)") if obs_cfg else \
+            "mdl_step (move+packages+env reward+MAPPO shaped reward+tracker+auto-reset)"
         out = {
             "metric": args.metric,
             "value": value,
             "unit": "agent-steps/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
+            "devices": devices,
+            "distinct_devices": len({d["pci"] for d in devices}),
+            "launcher": os.environ.get("MDL_BENCH_LAUNCHER", "torch.distributed.run" if dist is not None else "none"),
+            "process_group_backend": None if dist is None else dist.get_backend(),
             "steps": K,
             "warmup": args.warmup,
-            "graph_upload_replay_steps": 0 if graph is None else G,
-            "graph_steps": 0 if graph is None else G,
+            "graph_upload_replay_steps": 0 if args.no_graph else G,
+            "graph_steps": 0 if args.no_graph else G,
             "host_wait": args.host_wait if host_wait_rc in (None, 0) else f"{args.host_wait} (hipError {host_wait_rc})",
-            "ms_per_step": wall / K * 1e3,
+            "ms_per_step": ms_step,
+            "launch_floor_ms_per_step": None if floor is None else floor["ms_per_step"],
+            "over_floor_us": None if floor is None else (ms_step - floor["ms_per_step"]) * 1e3,
             "higher_is_better": True,
             "scaling": "strong" if args.total_envs > 0 else "weak",
             "vs_baseline": None,
-            "dtype": "int32+fp64",
+            "dtype": "int32+fp64" + (" (state, rewards) + f32 (observations)" if obs_cfg else ""),
             "data": "synthetic: uniform random trainer-int actions (Philox, on device), env seeds 42+global index",
             "config": {"workload": f"BASELINE config {args.config}: {'+'.join(args.maps)} A={A} P={P} T={args.T} "
-                                   f"{E} envs/GPU, mdl_step "
-                                   "(move+packages+env reward+MAPPO shaped reward+tracker+auto-reset), "
-                                   + ("eager launches" if graph is None else "hipGraph replay"),
+                                   f"{E} envs/GPU, {what}, "
+                                   + ("eager launches" if args.no_graph else "hipGraph replay"),
                        "envs_per_gpu": E, "total_envs": E_all, "agents": A, "packages": P, "max_time_steps": args.T,
                        "maps": args.maps, "map_runs_rank0": [[args.maps[m], b, n] for m, b, n in runs],
+                       "obs_dims": ({"actor_vec": env.actor_vec_dim, "critic_vec": env.critic_vec_dim,
+                                     "obs_bytes_per_env_step": obs_bytes_env} if obs_cfg else None),
                        "parallelism": f"env-shard x{world}"},
             "gpu_event_ms_per_step": gpu_ms / K,
             "eager": None if wall_eager is None else {"value": total_agent_steps / wall_eager,
                                                        "ms_per_step": wall_eager / K * 1e3},
+            "launch_floor": floor,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_over_algorithmic": None if traffic is None else traffic / per_launch_bytes,
                          "traffic_source": None if traffic_rec is None else traffic_rec.get("source"),
                          "kernel": kname, "kernel_us": kdur_us,
                          "kernel_us_isolated_event_pair": kdur_iso_us,
+                         "algorithmic_bytes_per_env_step": per_env,
                          "algorithmic_bytes_per_launch": per_launch_bytes},
             "fused_bench_mode": None if wall_f is None else {
                 "k_steps_per_launch": Kf, "launches": nf, "value": E_all * A * Kf * nf / wall_f,
@@ -416,12 +542,13 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_1thread": cpu1,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
     env.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -115,6 +115,12 @@ int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, 
 int mdl_step_fused(MdlEngine* eng, const uint8_t* actions, int32_t action_format, const int32_t* env_ids, int32_t n,
                    int32_t k_steps, int32_t auto_reset, double* r_env, float* r_shaped, uint8_t* done, void* stream);
 
+/* Measurement aid (no reference counterpart): the launch floor of mdl_step over n envs -- one
+ * launch of an EMPTY kernel with mdl_step's grid, workgroup size, LDS request and kernel-argument
+ * layout (so the same preloaded argument registers and kernarg segment).  bench.py replays it the
+ * way it replays mdl_step and reports the step's time above this floor.  Touches no state. */
+int mdl_step_floor(MdlEngine* eng, int32_t n, void* stream);
+
 /* ---- IDQ / qmix featurizers and IDQ reward shaping ----
  * mdl_build_obs_alt, for envs [env_begin, env_begin+n) sharing one map shape (H, W):
  *   idq_obs    f32 [n][A][6][H][W]       convert_state                IDQ/networks.py:112-217

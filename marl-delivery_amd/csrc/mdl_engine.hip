@@ -517,6 +517,15 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
     return 0;
 }
 
+int mdl_step_floor(MdlEngine* eng, int32_t n, void* stream) {
+    if (!eng) return fail("mdl_step_floor: null engine");
+    if (n < 1 || n > eng->p.E) return fail("mdl_step_floor: n=%d out of range", n);
+    DeviceGuard dg(eng->device);
+    HIPCHK(mdl::launch_step_floor(eng->p, n, step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step,
+                                  (hipStream_t)stream));
+    return 0;
+}
+
 int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, int32_t auto_reset, double* r_env,
                  float* r_shaped, uint8_t* done, float* actor_map, float* actor_vec, float* critic_map,
                  float* critic_vec, void* stream) {

@@ -1181,6 +1181,21 @@ __global__ __launch_bounds__(MDL_STEP_LB) void k_step_mail(const uint32_t* __res
                                                   inl ? ma.codes : act_pre, ap, nw, args, ObsArgs{}, &ma);
 }
 
+// mdl_step_floor: the launch floor of k_step -- the same kernel-argument layout (and so the
+// same preloaded SGPRs and kernarg segment size), workgroup size, LDS request and grid, and
+// no work.  bench.py replays it the way it replays the step (one graph node per step) and
+// reports the difference as the step's own cost above the dispatch floor.
+__global__ __launch_bounds__(MDL_STEP_LB) void k_step_floor(const uint32_t* __restrict__ rob_pre,
+                                                            const uint64_t* __restrict__ pkg_pre,
+                                                            const uint16_t* __restrict__ pst_pre,
+                                                            const u32x4* __restrict__ es_pre,
+                                                            const uint64_t* __restrict__ trk_pre,
+                                                            const uint8_t* __restrict__ act_pre, uint32_t ap,
+                                                            uint32_t nw, StepArgs args) {
+    (void)rob_pre, (void)pkg_pre, (void)pst_pre, (void)es_pre, (void)trk_pre, (void)act_pre, (void)ap, (void)nw;
+    (void)args;
+}
+
 // mdl_step_obs: k_step + k_obs_small in one launch (full batch, NCH = 1, A <= 8)
 template <bool STALE, int AU>
 __global__ __launch_bounds__(256) MDL_STEP_ATTR(1, false) void k_step_obs(const uint32_t* __restrict__ rob_pre,
@@ -1803,6 +1818,21 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
     else
         hipLaunchKernelGGL((k_step<ST, NCH, FUSED, 0>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
 #undef MDL_STEP_ARGS
+}
+
+hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s) {
+    StepArgs a{};
+    a.p = p;
+    a.n = n;
+    a.wpb = wpb;
+    a.lds_stride = (int)lds;
+    a.K = 1;
+    const dim3 grid(blocks_for(n, wpb)), block(64 * wpb);
+    const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
+    const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
+    hipLaunchKernelGGL(k_step_floor, grid, block, lds * wpb, s, p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk,
+                       (const uint8_t*)nullptr, ap, nw, a);
+    return hipGetLastError();
 }
 
 template <bool ST, bool FUSED>

@@ -16,6 +16,8 @@ hipError_t launch_reset(const DevParams& p, const int* ids, int n, int wpb, size
 hipError_t launch_tracker_clear(const DevParams& p, const int* ids, int n, hipStream_t s);
 hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
                        double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s);
+// the step's launch shape (grid, workgroup, LDS, kernel arguments) with an empty kernel
+hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s);
 hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int K,
                              int auto_reset, double* r, float* sh, uint8_t* done, int wpb, size_t lds,
                              hipStream_t s);

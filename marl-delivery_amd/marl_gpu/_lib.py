@@ -71,6 +71,7 @@ SIGNATURES = {
     "mdl_step": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mdl_step_obs": (C.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mdl_step_fused": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "mdl_step_floor": (C.c_int, [_vp, _i32, _vp]),
     "mdl_build_obs": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mdl_build_obs_alt": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp]),
     "mdl_views_alt_features": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp]),

@@ -326,6 +326,12 @@ class BatchedEnv:
         self._keep = (ids, actions)
         return r, sh, d
 
+    def step_floor(self, n: int | None = None):
+        """Measurement aid: one launch of an empty kernel in ``step``'s launch shape over n envs
+        (grid, workgroup, LDS, kernel arguments); touches no state.  bench.py's launch floor."""
+        n = self.E if n is None else int(n)
+        check(lib().mdl_step_floor(self._h, n, _raw_stream(self._dev)), "mdl_step_floor")
+
     def obs_buffers(self, n=None, H=None, W=None):
         n = self.E if n is None else n
         H = self.grids[0].shape[0] if H is None else H

@@ -22,6 +22,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define MT_N 624
 #define MT_M 397
@@ -793,6 +796,50 @@ void or_batch_step(OBatch* b, const uint8_t* actions_int, int auto_reset, const 
         if (mvp != mv) free(mvp);
         if (opp != op) free(opp);
     }
+}
+
+/* The observations the MAPPO rollout builds after every step (MAPPO/trainer.py:261-280):      */
+/* convert_global_state, then convert_observation and generate_vector_features per agent, of  */
+/* every env's current state and tracker.  Outputs [E][A][6][H][W], [E][A][Dv], [E][4][H][W], */
+/* [E][Dg]; any may be NULL.  The CPU leg of bench.py --config 3.                              */
+void or_batch_obs(OBatch* b, int T, int MO, int MP, int MR, int MPs, float* amap, float* avec, float* cmap,
+                  float* cvec, int n_threads) {
+    (void)n_threads;
+    const int A = b->A;
+    const int H = b->envs[0]->H, W = b->envs[0]->W, HW = H * W;
+    const size_t dv = 6 + 5 * (size_t)MO + 5 * (size_t)MP + 1, dg = 6 * (size_t)MR + 7 * (size_t)MPs + 1;
+    float* gm_scratch = (float*)malloc(sizeof(float) * 4 * (size_t)HW * (n_threads > 0 ? n_threads : 1));
+#pragma omp parallel for schedule(static) num_threads(n_threads > 0 ? n_threads : 1) if (n_threads > 1)
+    for (int e = 0; e < b->E; e++) {
+        const OEnv* env = b->envs[e];
+        const OTrk* k = b->trk[e];
+        int32_t rb[3 * 64];
+        int32_t* r1 = A <= 64 ? rb : (int32_t*)malloc(sizeof(int32_t) * 3 * (size_t)A);
+        env_robots1(env, r1);
+        float* gm = cmap ? cmap + (size_t)e * 4 * HW : NULL;
+        float* gv = cvec ? cvec + (size_t)e * dg : NULL;
+        if (gm || gv) {
+            int tid = 0;
+#ifdef _OPENMP
+            tid = omp_get_thread_num();
+#endif
+            float* gm_tmp = gm_scratch + (size_t)tid * 4 * HW;
+            float* gv_tmp = gv ? gv : (float*)malloc(sizeof(float) * dg);
+            or_convert_global_state(env->grid, H, W, env->t, A, r1, k->rows, k->n, T, MR, MPs, gm ? gm : gm_tmp,
+                                    gv_tmp);
+            if (!gv) free(gv_tmp);
+        }
+        for (int a = 0; a < A; a++) {
+            if (amap)
+                or_convert_observation(env->grid, H, W, env->t, A, r1, k->rows, k->n, a,
+                                       amap + ((size_t)e * A + a) * 6 * HW);
+            if (avec)
+                or_generate_vector_features(H, W, env->t, A, r1, k->rows, k->n, a, T, MO, MP,
+                                            avec + ((size_t)e * A + a) * dv);
+        }
+        if (r1 != rb) free(r1);
+    }
+    free(gm_scratch);
 }
 
 /* ----------------------------------------------------------------------- */

@@ -70,6 +70,7 @@ def lib():
         L.or_batch_trk.restype = vp
         L.or_batch_trk.argtypes = [vp, i32]
         L.or_batch_step.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32]
+        L.or_batch_obs.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32]
         L.or_idq_convert_state.argtypes = [vp, i32, i32, i32, i32, vp, vp, i32, i32, vp]
         L.or_qmix_global_tensor.argtypes = [vp, i32, i32, i32, i32, vp, vp, i32, i32, i32, vp]
         L.or_idq_reward_shaping.argtypes = [i32, vp, i32, vp, vp, i32, vp, i32, i32, vp]
@@ -254,6 +255,21 @@ class OracleBatch:
         d = np.zeros(self.E, np.uint8)
         lib().or_batch_step(self.h, _p(a), int(auto_reset), _p(cs), _p(r), _p(sh), _p(d), int(n_threads))
         return r, sh, d.astype(bool)
+
+    def obs(self, T, MO, MP, MR, MPs, out=None, n_threads=1):
+        """Every env's observations of its current state and tracker, as the MAPPO rollout builds
+        them after a step (MAPPO/trainer.py:261-280): dict of actor_map [E,A,6,H,W], actor_vec
+        [E,A,Dv], critic_map [E,4,H,W], critic_vec [E,Dg] (``out``: reuse these arrays)."""
+        E, A = self.E, self.A
+        H, W = self.grid.shape
+        if out is None:
+            out = dict(actor_map=np.zeros((E, A, 6, H, W), np.float32),
+                       actor_vec=np.zeros((E, A, 6 + 5 * MO + 5 * MP + 1), np.float32),
+                       critic_map=np.zeros((E, 4, H, W), np.float32),
+                       critic_vec=np.zeros((E, 6 * MR + 7 * MPs + 1), np.float32))
+        lib().or_batch_obs(self.h, int(T), MO, MP, MR, MPs, _p(out["actor_map"]), _p(out["actor_vec"]),
+                           _p(out["critic_map"]), _p(out["critic_vec"]), int(n_threads))
+        return out
 
 
 class OracleGreedy:

@@ -32,7 +32,8 @@ def test_bench_two_ranks_weak_scaling():
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["steps"] == 40
     assert d["config"]["total_envs"] == 1024 and d["config"]["envs_per_gpu"] == 512
     assert d["value"] > 0 and d["value"] == pytest.approx(1024 * 5 * 40 / (d["ms_per_step"] * 40 / 1e3), rel=1e-9)
-    assert d["cpu_baseline"] is None   # rank 0 at N = 1 only
+    assert d["cpu_baseline"] is None   # --cpu-seconds 0
+    assert d["ranks_seen"] == 2
 
 
 def test_bench_two_ranks_strong_scaling():
@@ -56,3 +57,47 @@ def test_bench_two_ranks_config5():
     assert d["config"]["agents"] == 16 and d["config"]["packages"] == 100 and d["config"]["envs_per_gpu"] == 512
     assert d["value"] > 0
 
+
+
+def _plain(args, timeout=300):
+    """bench.py as the driver's plain command (no torchrun around it)."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, cwd=REPO, env=env,
+                         capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout   # exactly rank 0's JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_plain_command_two_gpus_self_launches():
+    """`python3 bench.py --gpus 2 --backend gloo --steps 40 --warmup 5` as a plain
+    command starts torch.distributed.run itself; the line says how many ranks the process group saw,
+    which devices they ran on, and carries the CPU baseline (timed on rank 0 after the timed region)."""
+    d = _plain(["--gpus", "2", "--backend", "gloo", "--steps", "40", "--warmup", "5", "--cpu-seconds", "1",
+                "--fused-k", "0"])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["launcher"] == "self"
+    assert d["process_group_backend"] == "gloo"
+    assert sorted(x["rank"] for x in d["devices"]) == [0, 1] and all("gfx950" in x["arch"] for x in d["devices"])
+    assert d["distinct_devices"] == 1   # gloo rehearsal: both ranks share the box's one GPU
+    assert d["config"]["total_envs"] == 2 * 4096 and d["scaling"] == "weak"
+    cpu = d["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["host"]["nproc"] >= 1
+    assert d["cpu_baseline_1thread"]["threads_note"].startswith("single thread")
+    # the launch floor beside the step: an empty kernel in the step's launch shape
+    assert 0 < d["launch_floor_ms_per_step"] and d["over_floor_us"] == pytest.approx(
+        (d["ms_per_step"] - d["launch_floor_ms_per_step"]) * 1e3)
+
+
+def test_bench_one_gpu_launch_floor_and_config3_leg():
+    """The default line carries the launch floor; `--config 3` times mdl_step_obs (step + full
+    observations) with the write-bytes roofline and the CPU leg that builds the same observations."""
+    d = _plain(["--steps", "40", "--warmup", "5", "--cpu-seconds", "0", "--fused-k", "0"])
+    assert d["ranks_seen"] == 1 and d["launcher"] == "none" and d["launch_floor"]["ms_per_step"] > 0
+    assert d["launch_floor_ms_per_step"] < d["ms_per_step"]
+    d3 = _plain(["--config", "3", "--envs", "2048", "--steps", "20", "--warmup", "5", "--cpu-seconds", "0.5"])
+    assert d3["config"]["obs_dims"] == {"actor_vec": 52, "critic_vec": 1301, "obs_bytes_per_env_step": 19844}
+    assert d3["roofline"]["algorithmic_bytes_per_env_step"] == 19844 + 586
+    assert d3["roofline"]["kernel"] == "mdl::k_step_obs<true, 5>" and d3["launch_floor"] is None
+    assert d3["cpu_baseline"]["value"] > 0 and "full observations" in d3["cpu_baseline"]["sample"]

@@ -135,10 +135,59 @@ def test_product_has_no_oracle_dependency():
     assert "oracle" not in mk
 
 
-def test_bench_refuses_gpus_without_ranks():
-    """--gpus N needs N ranks: without torchrun the bench refuses instead of timing one GPU."""
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(_REPO, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_bench_gpus_n_self_launches_torchrun_without_touching_the_gpu(monkeypatch):
+    """`python bench.py --gpus 8 ...` outside torchrun: the parent starts
+    `python -m torch.distributed.run --nproc-per-node 8 bench.py <same args>` as a child and
+    returns its exit code, and makes no GPU call of its own (a GPU-initialising parent must not
+    spawn or exec GPU children on this pool)."""
+    import torch
+    bench = _bench_module()
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+
+    def no_gpu(*a, **k):
+        raise AssertionError("the launching parent touched the GPU")
+    for name in ("is_available", "init", "set_device", "synchronize", "current_device", "device_count"):
+        monkeypatch.setattr(torch.cuda, name, no_gpu)
+    seen = {}
+
+    def fake_forward(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+    monkeypatch.setattr(bench, "forward_child", fake_forward)
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    assert bench.main(argv) == 7
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-len(argv) - 1] == os.path.join(_REPO, "bench.py") and cmd[-len(argv):] == argv
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and seen["env"]["MDL_BENCH_LAUNCHER"] == "self"
+
+
+def test_bench_forward_child_passes_only_the_json_line(capfd):
+    """The self-launching parent forwards rank 0's JSON line to stdout, every other line of the
+    child to stderr, and the child's exit code."""
+    bench = _bench_module()
+    code = ("import json, sys; print('torchrun chatter'); print(json.dumps({'metric': 'm', 'value': 1})); "
+            "sys.stdout.flush(); sys.exit(3)")
+    assert bench.forward_child([sys.executable, "-c", code]) == 3
+    out, err = capfd.readouterr()
+    assert out.strip() == '{"metric": "m", "value": 1}' and "torchrun chatter" in err
+
+
+def test_bench_rank_count_must_match_gpus():
+    """Under torchrun (WORLD_SIZE set) --gpus must equal the rank count."""
+    env = dict(os.environ, WORLD_SIZE="1")
     out = subprocess.run([sys.executable, os.path.join(_REPO, "bench.py"), "--gpus", "2", "--steps", "5"], cwd=_REPO,
-                         capture_output=True, text=True, timeout=120)
+                         capture_output=True, text=True, timeout=120, env=env)
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
 
 

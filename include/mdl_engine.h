@@ -56,7 +56,15 @@ typedef struct {
     int32_t max_packages_obs;  /* MP */
     int32_t max_robots_state;  /* MR  (convert_global_state) */
     int32_t max_packages_state;/* MPs */
+    int32_t obs_builder;       /* MDL_OBS_BUILDER_*: which observation kernel mdl_build_obs uses (same outputs) */
 } MdlConfig;
+
+/* MdlConfig.obs_builder.  AUTO: the small builder (flat bit images, one tuple per lane) where it
+ * applies (A <= 8, P <= 64, 32-bit sort keys), the general builder otherwise.  GENERIC: always the
+ * general builder (any A, P).  Both produce the same floats; GENERIC exists so tests can compare
+ * the two on one configuration. */
+#define MDL_OBS_BUILDER_AUTO 0
+#define MDL_OBS_BUILDER_GENERIC 1
 
 /* Create an engine on `device`.  grids: n_maps row-major 0/1 maps packed back
  * to back; map_hw: 2*n_maps (H, W); env_map: E map indices (NULL = all map 0).

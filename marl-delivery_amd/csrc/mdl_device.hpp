@@ -131,12 +131,9 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 // neighbours or not) are touched by that XCD alone, launch after launch, and each launch finds
 // the rows the previous one wrote in that XCD's L2 (scripts/exp/l2_retain.hip: the state round
 // trip 1344 -> 1020 cycles at 4096 envs).  A bijection on [0, nb).
-#ifndef MDL_XCD_REMAP
-#define MDL_XCD_REMAP 1
-#endif
 __device__ __forceinline__ int xcd_slot(int b, int nb) { return (b & 7) * (nb >> 3) + min(b & 7, nb & 7) + (b >> 3); }
 __device__ __forceinline__ int xcd_block() {
-    return MDL_XCD_REMAP ? xcd_slot((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    return xcd_slot((int)blockIdx.x, (int)gridDim.x);
 }
 
 __device__ __forceinline__ void wave_sync() {

@@ -7,6 +7,7 @@
 #include "mdl_engine.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -163,6 +164,14 @@ struct MdlEngine {
         return (list_off + 2 * cap + cap + 15) & ~15;
     }
     bool has_greedy() const { return gstate != nullptr && !greedy_stale; }
+    // Every observation build goes through here: the env range must lie inside one run of
+    // same-shape envs (the small builder copies the rank table of the range's first env's map
+    // into LDS for the whole launch, mdl_obs_small.hpp k_obs_small; the outputs have one H x W).
+    hipError_t launch_obs(int env_begin, int n, float* am, float* av, float* cm, float* cv, hipStream_t s) const {
+        if (env_begin < 0 || n <= 0 || env_begin + n > p.E || shape_run_end[env_begin] < env_begin + n)
+            return hipErrorInvalidValue;
+        return mdl::launch_obs(p, env_begin, n, am, av, cm, cv, wpb_obs, lds_obs, s, obs_rank_lds);
+    }
 
     template <class T>
     int alloc(T** ptr, size_t count) {
@@ -429,7 +438,10 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) eng->n_cu = prop.multiProcessorCount;
     }
     p.obs_plane_words = mdl::obs_plane_words((int)A, eng->maxHW);
-    p.obs_small = mdl::obs_use_small((int)A, (int)P, p.key7_dsh, eng->maxHW, p.MO, p.MP) && !getenv("MDL_OBS_GENERIC");
+    if (c.obs_builder != MDL_OBS_BUILDER_AUTO && c.obs_builder != MDL_OBS_BUILDER_GENERIC)
+        return fail("unknown obs_builder %d", c.obs_builder);
+    p.obs_small = mdl::obs_use_small((int)A, (int)P, p.key7_dsh, eng->maxHW, p.MO, p.MP) &&
+                  c.obs_builder == MDL_OBS_BUILDER_AUTO;
     eng->lds_obs = p.obs_small ? mdl::obs_lds_small((int)A, eng->maxHW, (int)P, p.MO, p.MP)
                                : mdl::obs_lds((int)A, (int)P, eng->maxHW, p.MO, p.MP, p.MR, p.MPs);
     eng->wpb_obs = waves_per_block(eng->lds_obs);
@@ -437,16 +449,12 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     // (MO = MP = 100) 141-143 -> 135-137 us per build; with one pass (config 3) the block's table copy
     // and barrier cost more than the two gathers they save (74.5 -> 76 us; profiles/r04/obs_rank_lds_ab.txt)
     const int MPc_ = p.MP < (int)P ? p.MP : (int)P;
-    if (p.obs_small && MDL_OBS_RANK_LDS && (int)(A * A + A * MPc_ + A) > 64) {
+    if (p.obs_small && (int)(A * A + A * MPc_ + A) > 64) {
         for (int m = 0; m < n_maps; m++)
             eng->obs_rank_lds = std::max(eng->obs_rank_lds, (int)(((2 * eng->mapH[m] - 1) * (2 * eng->mapW[m] - 1) * 2 + 15) & ~15));
         // a workgroup's LDS: the table + wpb slices, within the per-CU budget of the builder's occupancy
         if ((size_t)eng->obs_rank_lds + eng->lds_obs * eng->wpb_obs > LDS_BUDGET || eng->obs_rank_lds > 8192)
             eng->obs_rank_lds = 0;
-    }
-    if (const char* v = getenv("MDL_OBS_WPB")) {   // profiling override (1..4 waves per workgroup)
-        const int x = atoi(v);
-        if (x >= 1 && x < eng->wpb_obs) eng->wpb_obs = x;
     }
     if (eng->wpb_step < 1 || eng->wpb_obs < 1) {
         delete eng;
@@ -550,8 +558,7 @@ int mdl_step_obs(MdlEngine* eng, const uint8_t* actions, int32_t action_format, 
     }
     HIPCHK(mdl::launch_step(eng->p, actions, action_format, nullptr, E, auto_reset, r_env, r_shaped, done,
                             step_wpb(E, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, s));
-    HIPCHK(mdl::launch_obs(eng->p, 0, E, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs, eng->lds_obs, s,
-                           eng->obs_rank_lds));
+    HIPCHK(eng->launch_obs(0, E, actor_map, actor_vec, critic_map, critic_vec, s));
     return 0;
 }
 
@@ -635,7 +642,12 @@ int mail_check_ids(MdlEngine* eng, int32_t n, int32_t use_ids, const char* who) 
 // system-scope release, by the final kernel of the call): no stream synchronisation, whose
 // wake-up costs microseconds more.  A failed launch never publishes, so the stream is asked now
 // and then.
+// The synchronous dict-API calls spin here (the callers hold the GIL: a call is microseconds to a
+// few milliseconds), so a GPU that never publishes must not hang the process: past
+// SPIN_LIMIT_S seconds with the stream still busy the call fails instead of spinning on.
+constexpr double SPIN_LIMIT_S = 60.0;
 int spin_wait(volatile const int32_t* seq, int32_t want, hipStream_t s, const char* who) {
+    const auto t0 = std::chrono::steady_clock::now();
     for (unsigned long spins = 1;; spins++) {
         if (*seq == want) return 0;
         __builtin_ia32_pause();
@@ -643,6 +655,9 @@ int spin_wait(volatile const int32_t* seq, int32_t want, hipStream_t s, const ch
             const hipError_t q = hipStreamQuery(s);
             if (q != hipSuccess && q != hipErrorNotReady) return fail("%s: %s", who, hipGetErrorString(q));
             if (q == hipSuccess && *seq != want) return fail("%s: the call finished without publishing", who);
+            const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (el > SPIN_LIMIT_S)
+                return fail("%s: no completion after %.0f s (stream still busy): giving up the wait", who, el);
         }
     }
 }
@@ -890,8 +905,7 @@ int mdl_build_obs(MdlEngine* eng, int32_t env_begin, int32_t n, float* actor_map
         return fail("mdl_build_obs: envs [%d, %d) mix map shapes (same-shape run ends at %d)", env_begin,
                     env_begin + n, eng->shape_run_end[env_begin]);
     DeviceGuard dg(eng->device);
-    HIPCHK(mdl::launch_obs(eng->p, env_begin, n, actor_map, actor_vec, critic_map, critic_vec, eng->wpb_obs,
-                           eng->lds_obs, (hipStream_t)stream, eng->obs_rank_lds));
+    HIPCHK(eng->launch_obs(env_begin, n, actor_map, actor_vec, critic_map, critic_vec, (hipStream_t)stream));
     return 0;
 }
 

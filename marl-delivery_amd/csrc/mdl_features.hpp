@@ -446,14 +446,11 @@ __device__ __forceinline__ float cvt_ub(uint32_t y) {
 // of cell `own`, 2 the bit row less `own` plus the multi-robot row), the float4 loop unrolled by
 // BITROWS_U: the unrolled group's LDS words are all read before the first is used and its stores
 // issue back to back (one kind branch per plane instead of per float4, one LDS wait per group).
-#ifndef MDL_BITROWS_U
-#define MDL_BITROWS_U 4
-#endif
 template <int KIND>
 __device__ __forceinline__ void bitrow_plane(GLOBAL char* base, const uint32_t* row, const uint32_t* mrow, int own,
                                              int qpp, int lane, uint32_t sh) {
     typedef float f32x4 __attribute__((ext_vector_type(4)));
-    constexpr int U = MDL_BITROWS_U;
+    constexpr int U = 4;   // float4 stores per unrolled group
     auto put = [&](int q, uint32_t b) {
         const uint32_t y = (b * 0x204081u) & 0x01010101u;   // bit i -> byte i (b < 16: no carries)
         *(GLOBAL f32x4*)(base + ((uint32_t)q << 4)) = f32x4{cvt_ub<0>(y), cvt_ub<1>(y), cvt_ub<2>(y), cvt_ub<3>(y)};
@@ -580,15 +577,13 @@ __host__ __device__ inline int actor_compact_dim(int A, int MO, int MPc) {
 __host__ __device__ inline int critic_compact_dim(int A, int MR, int MPsc) {
     return 6 * (A < MR ? A : MR) + 7 * MPsc + 1;
 }
-// agents whose compact actor rows are staged together (<= MDL_STAGE_FLOATS floats, >= 1 agent).
+// agents whose compact actor rows are staged together (<= STAGE_FLOATS floats, >= 1 agent).
 // The staging slice is most of the general builder's LDS per wave (config 5: 16 agents x 182 floats),
 // and that LDS sets its occupancy: 512 floats (2 agents there) leave the critic row as the largest
 // staged item (797 floats) and take the slice from 17.1 to 12.3 KB per wave.
-#ifndef MDL_STAGE_FLOATS
-#define MDL_STAGE_FLOATS 512
-#endif
+constexpr int STAGE_FLOATS = 512;
 __host__ __device__ inline int actor_group(int na, int Dc) {
-    const int g = MDL_STAGE_FLOATS / Dc;
+    const int g = STAGE_FLOATS / Dc;
     return g < 1 ? 1 : (g < na ? g : na);
 }
 

@@ -24,40 +24,11 @@
 #include "mdl_obs_small.hpp"
 #include "mdl_altfeat.hpp"
 
-// Profiling-only ablation builds (scripts/ablate.sh): bit 1 skips the shaped
+// Profiling-only ablation builds (MDL_PROFILING_BUILD, scripts/ablate.sh): bit 1 skips the shaped
 // reward, 2 the tracker update, 4 movement, 8 package actions, 16 the move-validity
 // reload, 32 the shaping agent loops, 64 the carried-package gather.  0 in the product.
-// Tracker update of the 16-robot kernel with the carried ids as an LDS bitmask (1) or readlanes (0)
-#ifndef MDL_TRK_LDS
-#define MDL_TRK_LDS 1
-#endif
-// Movement tests of the 16-robot kernel by lane groups and ds_bpermute (1) or by readlanes (0)
-#ifndef MDL_MOVE_PERM
-#define MDL_MOVE_PERM 1
-#endif
-// Sixteen-robot pick-ups (config 5) from an LDS bitmap of the pickers' cells: waiting packages
-// test their start cell against it, and only the packages that sit under a picker are walked
-// (usually none or one) instead of two ballots and ~20 scalar ops for every robot that tries
-#ifndef MDL_PICK_BITS
-#define MDL_PICK_BITS 1
-#endif
-// the general builder's maps straight from the cell bitsets (emit_maps_bitrows) when the
-// prebuilt plane words do not fit (64x64 maps)
-#ifndef MDL_OBS_BITROWS
-#define MDL_OBS_BITROWS 1
-#endif
-// Nearest waiting package of every agent from LDS-packed candidates (1) or one wave
-// reduction per agent (0) -- for the exact-A kernel of many robots (AU = 16, config 5:
-// 24.1 -> 22.1 us per step); with A <= 8 the LDS round trips on the latency-bound
-// path cost more than the reductions they replace (config 2 4.48 -> 4.60 us, measured)
-#ifndef MDL_NEAR_LDS
-#define MDL_NEAR_LDS 1
-#endif
 #ifndef MDL_ABLATE
 #define MDL_ABLATE 0
-#endif
-#ifndef MDL_COST_FOLD_TAB
-#define MDL_COST_FOLD_TAB 1
 #endif
 
 namespace mdl {
@@ -329,25 +300,18 @@ __global__ __launch_bounds__(256) void k_tracker_clear(DevParams p, const int* _
 // FUSED (bench mode): K consecutive steps of each env in
 // one launch with the state held in registers between them; actions [K][n][A],
 // outputs [K][n].  FUSED=false is the API's one step per launch (K = 1).
-#ifndef MDL_STEP_WPB
 // at most 4 waves per workgroup (the engine's step_wpb)
 #define MDL_STEP_LB 256
-#else
-#define MDL_STEP_LB (64 * MDL_STEP_WPB)
-#endif
 // Waves per SIMD the step kernels (k_step, k_step_obs) are compiled for.  Left to itself the
 // compiler spends 106 SGPRs, which allows 7 waves per SIMD; amdgpu_waves_per_eu(8) keeps the SGPRs
 // within the 8-wave budget at the same instruction count (+1 VALU).  Same-box A/B
 // (profiles/r03/wpe8_ab.txt): config 5 (131072 envs) 113.7 -> 99.5 us per step, its 16384-env slice
 // 16.6 -> 15.3, config 4 34.3 -> 31.5; config 2 (4 waves per SIMD) and k_step_obs unchanged;
-// the general builder k_obs 1.3 % slower with it, so it keeps the compiler's choice.  0: no attribute.
-#ifndef MDL_STEP_WPE
-#define MDL_STEP_WPE 8
-#endif
+// the general builder k_obs 1.3 % slower with it, so it keeps the compiler's choice.
 // Only the one- and two-chunk (P <= 128) per-launch forms: the fused bench kernel and the wider
 // package chunkings need more registers than the 8-wave budget and would spill (1 = no constraint).
 template <int NCH, bool FUSED>
-constexpr int step_wpe() { return (MDL_STEP_WPE > 0 && NCH <= 2 && !FUSED) ? MDL_STEP_WPE : 1; }
+constexpr int step_wpe() { return (NCH <= 2 && !FUSED) ? 8 : 1; }
 #define MDL_STEP_ATTR(NCH, FUSED) __attribute__((amdgpu_waves_per_eu(step_wpe<NCH, FUSED>())))
 // AU > 0: A <= AU robots (AU = 8, or AU = A exactly for the configs' A = 5 and 16) -- the
 // per-robot scans are unrolled over AU lanes (independent
@@ -386,7 +350,7 @@ constexpr uint32_t NW_IDS = 1u << 29, NW_MAP = 1u << 30;
 // fit: launch-order slots)
 constexpr int AP_NB_SHIFT = 18;
 inline uint32_t pack_ap(int A, int P, int nblocks) {
-    const uint32_t nb = (MDL_XCD_REMAP && nblocks < (1 << (32 - AP_NB_SHIFT))) ? (uint32_t)nblocks : 0u;
+    const uint32_t nb = nblocks < (1 << (32 - AP_NB_SHIFT)) ? (uint32_t)nblocks : 0u;
     return (uint32_t)A | ((uint32_t)P << 7) | (nb << AP_NB_SHIFT);
 }
 
@@ -618,7 +582,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
             // blocked: a lower-index mover proposes the same cell; occ: the robot
             // now standing on the proposed cell (robots stand on distinct cells)
             int blocked = 0, occ = -1;
-            if constexpr (AU == 16 && MDL_MOVE_PERM) {
+            if constexpr (AU == 16) {
                 // Sixteen robots: lane l tests robot i = l & 15 against robots j = 4g..4g+3
                 // (g = l >> 4, the lane group), fetched by ds_bpermute; the four groups' answers
                 // are combined so that lanes 0..15 end with robot i's -- 4 fetches instead of
@@ -721,7 +685,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
             }
             int cnew = carry;
             bool by_bits = false;
-            if constexpr (AU == 16 && MDL_PICK_BITS) {
+            if constexpr (AU == 16) {
                 const MapDesc& md = p.maps[mi];
                 if (md.H <= 64 && md.W <= 64) {   // cells (r, c) -> bit r * 64 + c of a 4096-bit map
                     by_bits = true;
@@ -791,11 +755,8 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
         double rr;
         if constexpr (AU > 0 && AU <= 8) {
             rr = p.cost_sum[n_cost];  // n_cost <= A <= 8: the same fold, tabulated on the host
-        } else if (MDL_COST_FOLD_TAB) {
-            rr = p.cost_fold[n_cost];  // n_cost <= A <= 64: likewise (one scalar load, no fp64 chain)
         } else {
-            rr = 0.0;
-            for (int k = 0; k < n_cost; k++) rr += p.move_cost;
+            rr = p.cost_fold[n_cost];  // n_cost <= A <= 64: likewise (one scalar load, no fp64 chain)
         }
         for (uint64_t m = dmask; m; m &= m - 1) {
             const int i = ffs64(m);
@@ -868,7 +829,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                 // order keys < 0x800, slots < 1024): the minimum names the nearest
                 // package with the reference's tie-break and carries its slot
                 uint64_t q = ballot(need_near || need_idle);
-                if constexpr (AU > 8 && MDL_NEAR_LDS) {
+                if constexpr (AU > 8) {
                     // Every agent at once: the waiting candidates of tracker_prev are packed
                     // into the wave's LDS slice (the reset scratch, unused until a reset below)
                     // as {start cell, key bits}; lane l scans every (64/AP)-th candidate for
@@ -971,7 +932,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
                     Midle = (sel && (kmin >> 21) <= 3u) ? ~0u : Midle;
                     best_cell = sel ? bc : best_cell;
                 }
-                for (uint64_t q = (AU > 8 && MDL_NEAR_LDS) ? 0ull : ballot(need_can); q; q &= q - 1) {
+                for (uint64_t q = AU > 8 ? 0ull : ballot(need_can); q; q &= q - 1) {
                     const int a = ffs64(q);
                     const int ca = rdl(cell, a);
                     uint64_t h = 0;
@@ -1027,7 +988,7 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
         // no pick-up, no drop and no spawn at t1 the update is a no-op, so it is skipped.
         if (STALE && !do_rst && !(MDL_ABLATE & 2) && (tookany | dmask | spawned))
         {
-            if constexpr (AU == 16 && MDL_TRK_LDS) {
+            if constexpr (AU == 16) {
                 // sixteen robots: the carried ids as a per-lane bitmask in the wave's LDS slice
                 // (free again: the shaping's candidates are consumed) -- one atomic OR per robot
                 // instead of 16 readlanes and 16 compares per package chunk
@@ -1287,7 +1248,7 @@ __global__ __launch_bounds__(256) void k_obs(DevParams p, int env_begin, int n, 
             feat_build_planes(c, L, planes);
             if (am) emit_planes(planes, c.NW, 6 * A, c.HW, am);
             if (cm) emit_planes(planes + 6 * A * c.NW, c.NW, 4, c.HW, cm);
-        } else if (MDL_OBS_BITROWS && (c.HW & 3) == 0 && (((uintptr_t)am | (uintptr_t)cm) & 15) == 0 && (am || cm)) {
+        } else if ((c.HW & 3) == 0 && (((uintptr_t)am | (uintptr_t)cm) & 15) == 0 && (am || cm)) {
             emit_maps_bitrows(L, c.NW, c.HW, A, am, cm);
         } else {
             if (am) emit_actor_maps(c, L, 0, A, true, am);
@@ -1785,9 +1746,6 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
                           double* r, float* sh, uint8_t* done, int wpb, size_t lds, int K, hipStream_t s) {
     // n and wpb travel packed in one preloaded dword (n < 2^24, wpb < 32; the engine
     // checks both at creation)
-#ifdef MDL_STEP_WPB  // profiling builds only: workgroup shape experiments
-    wpb = MDL_STEP_WPB;
-#endif
     const int threads = 64 * wpb;
 #ifdef MDL_EXP_NOLDS  // profiling builds only: no LDS request (valid only while no env resets)
     lds = 0;

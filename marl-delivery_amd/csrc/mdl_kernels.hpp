@@ -24,11 +24,10 @@ hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt
 hipError_t launch_step_obs(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
                            float* sh, uint8_t* done, float* amap, float* avec, float* cmap, float* cvec, int wpb,
                            size_t lds, hipStream_t s);
-#ifndef MDL_OBS_RANK_LDS
-#define MDL_OBS_RANK_LDS 1
-#endif
 // rank_lds > 0 (small builder): bytes of LDS in front of the per-wave slices holding the launch's
-// distance-rank table (mdl_obs_small.hpp k_obs_small)
+// distance-rank table (mdl_obs_small.hpp k_obs_small).  PRECONDITION: envs [env_begin, env_begin+n)
+// share one map shape -- the table copied is env_begin's map's.  The engine checks it
+// (MdlEngine::launch_obs, mdl_engine.hip) before every call.
 hipError_t launch_obs(const DevParams& p, int env_begin, int n, float* amap, float* avec, float* cmap, float* cvec,
                       int wpb, size_t lds, hipStream_t s, int rank_lds = 0);
 // A launch's own completion word (host-mapped): every wave of its grid counts itself in the

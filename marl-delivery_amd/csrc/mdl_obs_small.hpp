@@ -19,29 +19,14 @@
 #pragma once
 #include "mdl_features.hpp"
 
-// Early whole-slab zero fill of mostly-padding vectors: bit 1 actor vectors, bit 2
-// critic vectors (see k_obs_small).  Measured (scripts/exp/earlyfill.sh, 16384 envs):
-// the 1007-dim actor vectors 138-152 -> 122-124 us per build; the critic vector's
-// early fill was slower (136-169 us with both bits), so only bit 1 is on.
-#ifndef MDL_OBS_EARLYFILL
-#define MDL_OBS_EARLYFILL 1
-#endif
+// Early whole-slab zero fill of mostly-padding actor vectors (see k_obs_small).  Measured
+// (scripts/exp/earlyfill.sh, 16384 envs): the 1007-dim actor vectors 138-152 -> 122-124 us per
+// build; the same early fill of the critic vector was slower (136-169 us), so it has none.
 // Single-write actor vectors (mostly-padding vectors, e.g. the 1007-dim one): the tuples are
 // assembled in an LDS image of each agent's data slots and the env's whole actor-vector slab
 // is then streamed once as aligned float4s -- data float4s from the image, padding float4s as
 // zeros -- instead of a zero-filled slab overwritten by the tuples after a vmcnt(0) wait
 // (which wrote the tuple bytes twice).  Replaces the early fill when it applies.
-// Single-write streaming loops with clamped lane indices instead of per-iteration exec masks (1)
-#ifndef MDL_OBS_CLAMP
-#define MDL_OBS_CLAMP 1
-#endif
-#ifndef MDL_OBS_SINGLEWRITE
-#define MDL_OBS_SINGLEWRITE 1
-#endif
-// Package order for a few slots by all agents' minima at once (wave_min8_u32)
-#ifndef MDL_OBS_MIN8
-#define MDL_OBS_MIN8 1
-#endif
 
 namespace mdl {
 
@@ -256,7 +241,7 @@ constexpr int OBS_SW_TAB = 16 * 2 * 8 + 16 * 3 * 8;   // bytes: [17] (q0, base) 
 // aligned output, else it takes the early-fill path, which fits the same LDS slice).
 __host__ __device__ inline bool obs_sw_config(int A, int P, int MO, int MP) {
     const int MOc = MO < A - 1 ? MO : A - 1, MPc = MP < P ? MP : P;
-    return MDL_OBS_SINGLEWRITE && (MO > MOc || MP > MPc);
+    return MO > MOc || MP > MPc;
 }
 __host__ __device__ inline size_t obs_small_lds(int A, int HW, int P, int MO, int MP) {
     const int MOc = MO < A - 1 ? MO : A - 1, MPc = MP < P ? MP : P;
@@ -319,10 +304,8 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
     // later, after an s_waitcnt vmcnt(0) (stores count in vmcnt on gfx9: the
     // zeros have reached L2 before any overwrite is issued).
     const bool sw = avec && obs_sw_config(A, P, MO, MP) && (((uintptr_t)avec & 15) == 0);
-    const bool av_early = !sw && (MDL_OBS_EARLYFILL & 1) && avec && (MO > MOc || MP > MPc);
-    const bool cv_early = (MDL_OBS_EARLYFILL & 2) && cvec && (MR > A || MPs > P);
+    const bool av_early = !sw && avec && (MO > MOc || MP > MPc);
     if (av_early) zero_fill(avec + (size_t)w * A * (6 + 5 * MO + 5 * MP + 1), A * (6 + 5 * MO + 5 * MP + 1));
-    if (cv_early) zero_fill(cvec + (size_t)w * (6 * MR + 7 * MPs + 1), 6 * MR + 7 * MPs + 1);
 
     // ---- tracker view of each slot (TrkStale / TrkFresh) ----
     // ord7: the dict order as 7 bits -- survivors of earlier episodes by their
@@ -443,7 +426,7 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
 #pragma unroll
             for (int a = 0; a < 5; a++)
                 if (lane < want) invp[a * 64 + lane] = o2j[k5[a] & 127u];
-        } else if (want <= 6 && MDL_OBS_MIN8) {
+        } else if (want <= 6) {
             // a few slots: repeated wave minima (keys are unique), all agents' at once by the
             // halving transpose (wave_min8_u32: ~20 VALU per slot for every agent instead of a
             // 6-stage DPP chain per agent)
@@ -615,7 +598,6 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
             // at its last, so every gap float4 lies inside the slab.
             wave_sync();
             float4* a4 = reinterpret_cast<float4*>(avec);
-#if MDL_OBS_CLAMP
             // The slab's two end float4s may hold a neighbouring env's floats: written per float
             // by two lanes; every other float4 by uniform-trip loops in which lanes past a run's end
             // repeat its last float4 (the same value: no exec-mask branches per iteration).
@@ -645,26 +627,6 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
                 for (int q0 = wt.y; q0 < gend; q0 += WAVE)   // uniform
                     a4[min(q0 + lane, gend - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
-#else
-            for (int wi = 0; wi < nwin; wi++) {   // uniform
-                const int4 wt = wtab[wi];
-                for (int q = wt.x + lane; q < wt.y; q += WAVE) {
-                    const float4 v = img4[wt.z + (q - wt.x)];
-                    const int f0 = 4 * q - g0;   // slab-relative index of the float4's first float
-                    if (f0 >= 0 && f0 + 4 <= S) {
-                        a4[q] = v;
-                    } else {
-                        float* d = avec + 4 * (size_t)q;
-                        if ((unsigned)f0 < (unsigned)S) d[0] = v.x;
-                        if ((unsigned)(f0 + 1) < (unsigned)S) d[1] = v.y;
-                        if ((unsigned)(f0 + 2) < (unsigned)S) d[2] = v.z;
-                        if ((unsigned)(f0 + 3) < (unsigned)S) d[3] = v.w;
-                    }
-                }
-                const int gend = wi + 1 < nwin ? wtab[wi + 1].x : wt.y;
-                for (int q = wt.y + lane; q < gend; q += WAVE) a4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            }
-#endif
         }
         // padding: other-robot slots [MOc, MO) and package slots [ns, MP) of every agent
         if (!sw && !av_early && (MO > MOc || MP > ns)) {
@@ -681,7 +643,6 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
         float* cv = cvec + (size_t)w * Dg;
         const int nr = A < MR ? A : MR;
         const int npr = nact < MPsc ? nact : MPsc;
-        if (cv_early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slab's zeros are in L2
         for (int q0 = 0; q0 < nr + npr; q0 += WAVE) {   // uniform trip count: bperm needs every lane
             const int q = q0 + lane;
             const bool isr = q < nr, live = q < nr + npr;
@@ -714,10 +675,8 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
                 if (!isr) o[6] = d6;
             }
         }
-        if (!cv_early) {
-            zero_fill(cv + 6 * nr, 6 * (MR - nr));
-            zero_fill(cv + 6 * MR + 7 * npr, 7 * (MPs - npr));
-        }
+        zero_fill(cv + 6 * nr, 6 * (MR - nr));
+        zero_fill(cv + 6 * MR + 7 * npr, 7 * (MPs - npr));
         if (lane == 0) cv[Dg - 1] = qdiv_r(t, yT);
     }
 }

@@ -30,6 +30,8 @@ MDL_ACTION_TRAINER_INT = 0
 MDL_ACTION_CODES = 1
 MDL_MAX_ROBOTS = 64
 MDL_MAX_PACKAGES = 1024
+MDL_OBS_BUILDER_AUTO = 0
+MDL_OBS_BUILDER_GENERIC = 1
 
 
 class MdlConfig(C.Structure):
@@ -48,6 +50,7 @@ class MdlConfig(C.Structure):
         ("max_packages_obs", C.c_int32),
         ("max_robots_state", C.c_int32),
         ("max_packages_state", C.c_int32),
+        ("obs_builder", C.c_int32),
     ]
 
 

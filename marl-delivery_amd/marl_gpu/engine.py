@@ -32,6 +32,7 @@ QMIX_SHAPING = (0.5, 2.0, 0.2, 0.02, -0.1, -0.1, -0.05, -0.02, -0.02)
 TRACKER_MODES = {"fresh": _lib.MDL_TRACKER_FRESH, "mappo": _lib.MDL_TRACKER_MAPPO_STALE,
                  "mappo_stale": _lib.MDL_TRACKER_MAPPO_STALE}
 ACTION_FORMATS = {"int": _lib.MDL_ACTION_TRAINER_INT, "codes": _lib.MDL_ACTION_CODES}
+OBS_BUILDERS = {"auto": _lib.MDL_OBS_BUILDER_AUTO, "generic": _lib.MDL_OBS_BUILDER_GENERIC}
 STATUS_NAMES = ("None", "waiting", "in_transit", "delivered")
 
 
@@ -54,7 +55,9 @@ class BatchedEnv:
     shaping:   "mappo" | "qmix" | 9 constants;
     obs dims:  max_other_robots / max_packages_obs (generate_vector_features),
                max_robots_state / max_packages_state (convert_global_state);
-               obs_max_time_steps defaults to max_time_steps.
+               obs_max_time_steps defaults to max_time_steps;
+    obs_builder:   "auto" (the small builder where it applies, A <= 8 and P <= 64) or
+               "generic" (always the general builder): the same observations either way.
     After construction every env holds the constructor's layout draw; call
     ``reset()`` for the first episode, as the reference trainers do.
     """
@@ -64,7 +67,7 @@ class BatchedEnv:
                  seed: int = 2025, seeds: Sequence[int] | None = None, env_map: Sequence[int] | None = None,
                  tracker: str = "mappo", shaping="mappo", max_other_robots: int | None = None,
                  max_packages_obs: int = 5, max_robots_state: int = 100, max_packages_state: int = 100,
-                 obs_max_time_steps: int | None = None, device=None):
+                 obs_max_time_steps: int | None = None, obs_builder: str = "auto", device=None):
         if not torch.cuda.is_available():
             raise RuntimeError("marl_gpu.BatchedEnv needs a ROCm GPU (no CPU fallback)")
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
@@ -93,6 +96,7 @@ class BatchedEnv:
         cfg.obs_max_time_steps = self.obs_T
         cfg.max_other_robots, cfg.max_packages_obs = self.MO, self.MP
         cfg.max_robots_state, cfg.max_packages_state = self.MR, self.MPs
+        cfg.obs_builder = OBS_BUILDERS[obs_builder]
         self.cfg = cfg
         flat = np.ascontiguousarray(np.concatenate([g.reshape(-1) for g in self.grids]).astype(np.uint8))
         hw = np.array([[g.shape[0], g.shape[1]] for g in self.grids], np.int32).reshape(-1)

@@ -22,13 +22,9 @@ def _mg():
 
 
 def _pair(mg, g, E, A, P, T, **kw):
-    """Two engines with identical streams: the small builder and (MDL_OBS_GENERIC) the generic one."""
+    """Two engines with identical streams: the small builder and the generic one (MdlConfig.obs_builder)."""
     a = mg.BatchedEnv(g, E, A, P, T, **kw)
-    os.environ["MDL_OBS_GENERIC"] = "1"
-    try:
-        b = mg.BatchedEnv(g, E, A, P, T, **kw)
-    finally:
-        del os.environ["MDL_OBS_GENERIC"]
+    b = mg.BatchedEnv(g, E, A, P, T, obs_builder="generic", **kw)
     return a, b
 
 

@@ -305,3 +305,22 @@ def test_traffic_json_recomputes_from_committed_profiles(tmp_path):
     for a, b in zip(tj["records"], again["records"]):
         assert a["hbm_bytes_per_launch"] == b["hbm_bytes_per_launch"], a["name"]
         assert a["fetch_dispatches"] == b["fetch_dispatches"] >= 100
+
+
+def test_product_sources_have_no_variant_switches():
+    """the product kernels carry no compile-time A/B switches (the non-default
+    branches of round 4's experiments are deleted; the history keeps them) and read no environment
+    overrides.  The only preprocessor switches left are the profiling-only ones, each an #error
+    without -DMDL_PROFILING_BUILD (test_profiling_switches_need_a_profiling_build)."""
+    fenced = {"MDL_EXP_NOWAIT", "MDL_EXP_NOTUPLES", "MDL_EXP_NOLDS", "MDL_ABLATE", "MDL_STAMPS", "MDL_PROFILING_BUILD"}
+    srcs = [os.path.join(REPO, "marl-delivery_amd", "csrc", f) for f in os.listdir(os.path.join(REPO, "marl-delivery_amd", "csrc"))]
+    srcs.append(os.path.join(REPO, "include", "mdl_engine.h"))
+    seen = set()
+    for path in srcs:
+        txt = open(path).read()
+        assert "getenv" not in txt, path
+        for m in re.finditer(r"^\s*#\s*(?:if|ifdef|ifndef|elif)\b(.*)$", txt, re.M):
+            for name in re.findall(r"\b(MDL_[A-Z0-9_]+)", m.group(1)):
+                seen.add(name)
+                assert name in fenced or name == "MDL_ENGINE_H", (path, m.group(0))
+    assert {"MDL_ABLATE", "MDL_STAMPS"} <= seen

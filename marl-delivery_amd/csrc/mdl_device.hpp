@@ -24,6 +24,14 @@
      defined(MDL_STAMPS))
 #error "MDL_EXP_NOWAIT / MDL_EXP_NOTUPLES / MDL_EXP_NOLDS / MDL_ABLATE / MDL_STAMPS need -DMDL_PROFILING_BUILD"
 #endif
+// Profiling-only ablation builds (MDL_PROFILING_BUILD, scripts/ablate.sh): bit 1 skips the shaped
+// reward, 2 the tracker update, 4 movement, 8 package actions, 16 the move-validity reload, 32 the
+// shaping agent loops, 64 the carried-package gather; in the small observation builder 128 the
+// actor vectors' computation, 256 the critic vector's, 512 the map planes' (their bytes are still
+// written).  0 in the product.
+#ifndef MDL_ABLATE
+#define MDL_ABLATE 0
+#endif
 
 namespace mdl {
 

@@ -24,12 +24,6 @@
 #include "mdl_obs_small.hpp"
 #include "mdl_altfeat.hpp"
 
-// Profiling-only ablation builds (MDL_PROFILING_BUILD, scripts/ablate.sh): bit 1 skips the shaped
-// reward, 2 the tracker update, 4 movement, 8 package actions, 16 the move-validity
-// reload, 32 the shaping agent loops, 64 the carried-package gather.  0 in the product.
-#ifndef MDL_ABLATE
-#define MDL_ABLATE 0
-#endif
 
 namespace mdl {
 

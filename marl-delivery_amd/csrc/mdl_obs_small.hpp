@@ -445,19 +445,6 @@ __device__ __forceinline__ void obs_small_emit(const DevParams& p, int w, int mi
                     }
                 }
             }
-        } else if (want <= 6) {
-            // a few slots: repeated wave minima (keys are unique)
-            for (int s = 0; s < want; s++) {
-#pragma unroll
-                for (int a = 0; a < 8; a++) {
-                    if (a < A) {
-                        const uint32_t m = wave_min_u32(key[a]);
-                        const bool hit = key[a] == m;
-                        if (hit) invp[a * 64 + s] = (uint8_t)lane;
-                        key[a] = hit ? 0xffffffffu : key[a];
-                    }
-                }
-            }
         } else {
 #pragma unroll
             for (int a = 0; a < 8; a++) {

@@ -1,9 +1,11 @@
 """Write profiles/traffic.json (the roofline.traffic source bench.py reads) from rocprofv3 PMC
 passes of the current build, corrected by the committed FETCH_SIZE calibration.
 
-Usage: python scripts/traffic_json.py OUT.json CAL.json NAME=DIR[:config] ...
-  DIR holds fetch/ and write/ rocprofv3 CSV passes (run_counter_collection.csv) of k_step;
-  config = envs,agents,packages,map1+map2... (default 4096,5,50,map1.txt).
+Usage: python scripts/traffic_json.py OUT.json CAL.json NAME=DIR[:config[:kernel[:obs]]] ...
+  DIR holds fetch/ and write/ rocprofv3 CSV passes (run_counter_collection.csv) of the kernel;
+  config = envs,agents,packages,map1+map2... (default 4096,5,50,map1.txt); kernel = the kernel-name
+  substring (default k_step); obs = 1 for a step + observation launch (bench.py --config 3), whose
+  reads are the step's (the same calibrated access shapes) and whose writes are mostly observations.
 Counter values are KB (x1024).  HBM bytes per launch = FETCH_SIZE x (1 / the calibrated
 counted-over-read ratio of the step's access shape) + WRITE_SIZE (exact for the writes, per
 the calibration's write column)."""
@@ -41,17 +43,21 @@ def main():
     recs = []
     for spec in sys.argv[3:]:
         name, rest = spec.split("=", 1)
-        d, _, cfg = rest.partition(":")
+        d, _, more = rest.partition(":")
+        cfg, _, more = more.partition(":")
+        kern, _, obs = more.partition(":")
+        kern = kern or "k_step"
         E, A, P, maps = (cfg or "4096,5,50,map1.txt").split(",")
-        fetch, nf = median_counter(os.path.join(d, "fetch"), "FETCH_SIZE", "k_step")
-        write, nw = median_counter(os.path.join(d, "write"), "WRITE_SIZE", "k_step")
+        fetch, nf = median_counter(os.path.join(d, "fetch"), "FETCH_SIZE", kern)
+        write, nw = median_counter(os.path.join(d, "write"), "WRITE_SIZE", kern)
         if fetch is None or write is None:
-            raise SystemExit(f"{name}: no FETCH_SIZE / WRITE_SIZE rows for k_step under {d}")
+            raise SystemExit(f"{name}: no FETCH_SIZE / WRITE_SIZE rows for {kern} under {d}")
         read_bytes = fetch / ratio
         recs.append({
             "name": name,
             "config": {"envs": int(E), "agents": int(A), "packages": int(P), "maps": maps.split("+")},
-            "kernel": "mdl::k_step",
+            "kernel": "mdl::" + kern,
+            "obs": obs == "1",
             "hbm_bytes_per_launch": read_bytes + write,
             "fetch_size_bytes_median": fetch, "fetch_dispatches": nf,
             "read_bytes_corrected": read_bytes,

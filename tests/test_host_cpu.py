@@ -297,7 +297,7 @@ def test_traffic_json_recomputes_from_committed_profiles(tmp_path):
         assert src.startswith("profiles/") and os.path.isdir(os.path.join(REPO, src)), src
         c = rec["config"]
         specs.append(f"{rec['name']}={os.path.join(REPO, src)}:{c['envs']},{c['agents']},{c['packages']},"
-                     + "+".join(c["maps"]))
+                     + "+".join(c["maps"]) + f":{rec['kernel'].replace('mdl::', '')}:{int(bool(rec.get('obs')))}")
     out = tmp_path / "traffic.json"
     subprocess.check_call([sys.executable, os.path.join(REPO, "scripts", "traffic_json.py"), str(out),
                            os.path.join(REPO, tj["calibration"])] + specs, stdout=subprocess.DEVNULL)

@@ -20,6 +20,9 @@ DST = os.path.join(REPO, "profiles", "r05", "final")
 PMC = {"c2": ("k_step<", ":4096,5,50,map1.txt:k_step<:0"),
        "c3": ("k_step_obs", ":16384,5,50,map1.txt:k_step_obs:1"),
        "c5": ("k_step<", ":16384,16,100,synthetic64.txt:k_step<:0")}
+# full-size launches of bench.py --config 4 / --config 5 (scripts/profile_r05_full.sh): FETCH_SIZE / WRITE_SIZE only
+PMC_FULL = {"c4": ("k_step<", ":65536,5,50," + "+".join(f"map{i}.txt" for i in range(1, 6)) + ":k_step<:0"),
+            "c5full": ("k_step<", ":131072,16,100,synthetic64.txt:k_step<:0")}
 
 
 def one(pattern):
@@ -67,6 +70,11 @@ def main():
                 wv = m.get("SQ_WAVES", 1.0)
                 summary.append(f"{cfg} {kern} per wave (medians over dispatches): " +
                                json.dumps({n: round(v / wv, 1) for n, v in sorted(m.items())}))
+    for cfg, (kern, _) in PMC_FULL.items():
+        for kind in ("fetch", "write"):
+            if not trim_pmc(os.path.join(SRC, cfg, kind), os.path.join(DST, "pmc", cfg, kind, "run_counter_collection.csv"),
+                            kern):
+                raise SystemExit(f"no {kern} rows in {cfg}/{kind}")
     for f in stats.values():
         for r in csv.DictReader(open(os.path.join(DST, f))):
             if r["Name"].startswith("void mdl::") or r["Name"].startswith("mdl::"):
@@ -77,7 +85,7 @@ def main():
                        f"{d['roofline']['kernel_us']:.3f} frac {d['roofline']['frac']:.4f} "
                        f"launch_floor_ms_per_step {d.get('launch_floor_ms_per_step')}")
     open(os.path.join(DST, "profile_summary.txt"), "w").write("\n".join(summary) + "\n")
-    specs = [f"{cfg}=" + os.path.join(DST, "pmc", cfg) + suffix for cfg, (_, suffix) in PMC.items()]
+    specs = [f"{cfg}=" + os.path.join(DST, "pmc", cfg) + suffix for cfg, (_, suffix) in {**PMC, **PMC_FULL}.items()]
     subprocess.check_call([sys.executable, os.path.join(REPO, "scripts", "traffic_json.py"),
                            os.path.join(REPO, "profiles", "traffic.json"),
                            os.path.join(REPO, "profiles", "r03", "fetch_calibration.json")] + specs,

@@ -95,6 +95,9 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="eager launches only (PMC profiling passes)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend under torchrun (gloo: rehearse N ranks on fewer GPUs)")
+    ap.add_argument("--step-layout", default="auto", choices=("auto", "wave", "rows"),
+                    help="mdl_step's env-to-wavefront mapping (MdlConfig.step_layout; same results): auto = four "
+                         "envs per wavefront where A <= 8 and P <= 64")
     ap.add_argument("--host-wait", default="auto", choices=("auto", "spin", "yield", "blocking"),
                     help="how the host waits for the GPU in synchronize (hipSetDeviceFlags schedule mode)")
     ap.add_argument("--graph-only", action="store_true",
@@ -295,7 +298,7 @@ def main(argv=None):
     obs_cfg = args.config == "3"
     obs_dims = OBS5 if args.config == "5" else OBS3
     env = marl_gpu.BatchedEnv(grids if len(grids) > 1 else grids[0], E, A, P, args.T, seeds=seeds, env_map=env_map,
-                              tracker="mappo", shaping="mappo", device=dev, **obs_dims)
+                              tracker="mappo", shaping="mappo", device=dev, step_layout=args.step_layout, **obs_dims)
     env.reset()
 
     G = max(1, min(args.graph_steps, args.steps))
@@ -462,7 +465,9 @@ def main(argv=None):
                 tj = json.load(open(args.traffic_json))
                 want = {"envs": E, "agents": A, "packages": P, "maps": args.maps}
                 for rec in tj.get("records", []):
-                    if rec.get("config") == want and bool(rec.get("obs")) == obs_cfg:
+                    rows_rec = "k_step_rows" in rec.get("kernel", "")
+                    if rec.get("config") == want and bool(rec.get("obs")) == obs_cfg and \
+                            (obs_cfg or rows_rec == env.step_rows):   # the PMC pass of the kernel timed here
                         traffic, traffic_rec = rec.get("hbm_bytes_per_launch"), rec
             except (OSError, ValueError):
                 traffic = None
@@ -479,6 +484,9 @@ def main(argv=None):
         kname = {"2": "mdl::k_step<true, 1, false, 5>", "3": "mdl::k_step_obs<true, 5>",
                  "4": "mdl::k_step<true, 1, false, 5> (mixed maps)",
                  "5": "mdl::k_step<true, 2, false, 16>"}[args.config] if std else "mdl::k_step"
+        if env.step_rows and args.config != "3":
+            kname = "mdl::k_step_rows<true, 5>" if A == 5 else "mdl::k_step_rows<true, 8>"
+            kname += " (mixed maps)" if args.config == "4" else ""
         ms_step = wall / K * 1e3
         floor = None
         if wall_floor is not None:
@@ -521,7 +529,8 @@ def main(argv=None):
                        "maps": args.maps, "map_runs_rank0": [[args.maps[m], b, n] for m, b, n in runs],
                        "obs_dims": ({"actor_vec": env.actor_vec_dim, "critic_vec": env.critic_vec_dim,
                                      "obs_bytes_per_env_step": obs_bytes_env} if obs_cfg else None),
-                       "parallelism": f"env-shard x{world}"},
+                       "parallelism": f"env-shard x{world}",
+                       "step_layout": "rows (4 envs per wavefront)" if env.step_rows else "wave (1 env per wavefront)"},
             "gpu_event_ms_per_step": gpu_ms / K,
             "eager": None if wall_eager is None else {"value": total_agent_steps / wall_eager,
                                                        "ms_per_step": wall_eager / K * 1e3},

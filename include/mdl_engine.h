@@ -57,6 +57,7 @@ typedef struct {
     int32_t max_robots_state;  /* MR  (convert_global_state) */
     int32_t max_packages_state;/* MPs */
     int32_t obs_builder;       /* MDL_OBS_BUILDER_*: which observation kernel mdl_build_obs uses (same outputs) */
+    int32_t step_layout;       /* MDL_STEP_LAYOUT_*: how mdl_step maps envs onto wavefronts (same outputs) */
 } MdlConfig;
 
 /* MdlConfig.obs_builder.  AUTO: the small builder (flat bit images, one tuple per lane) where it
@@ -65,6 +66,16 @@ typedef struct {
  * the two on one configuration. */
 #define MDL_OBS_BUILDER_AUTO 0
 #define MDL_OBS_BUILDER_GENERIC 1
+
+/* MdlConfig.step_layout.  ROWS: a full-batch mdl_step (env_ids NULL) runs four envs per wavefront,
+ * one per 16-lane row (A <= 8, P <= 64; mdl_create fails otherwise).  WAVE: one env per wavefront
+ * always.  AUTO: ROWS where it applies and the batch has at least 10,240 envs (where it is the
+ * faster of the two on MI355X), WAVE otherwise.  Subset steps (env_ids), mdl_step_fused,
+ * mdl_step_obs and the mailbox step always use one wave per env.  Every layout produces the same
+ * state and outputs; WAVE / ROWS exist so tests can compare the two on one configuration. */
+#define MDL_STEP_LAYOUT_AUTO 0
+#define MDL_STEP_LAYOUT_WAVE 1
+#define MDL_STEP_LAYOUT_ROWS 2
 
 /* Create an engine on `device`.  grids: n_maps row-major 0/1 maps packed back
  * to back; map_hw: 2*n_maps (H, W); env_map: E map indices (NULL = all map 0).

@@ -118,6 +118,17 @@ struct MdlEngine {
     std::vector<int> mapH, mapW;
     std::vector<void*> allocs;
     size_t lds_step = 0, lds_obs = 0;
+    bool step_rows = false;   // k_step_rows applies (A <= 8, P <= 64) and the layout allows it
+    bool rows_forced = false; // MDL_STEP_LAYOUT_ROWS: at every batch size
+    size_t lds_rows = 0;
+    // Whether a full-batch step over n envs runs four envs per wavefront.  AUTO: from ROWS_MIN_ENVS
+    // envs on.  Below that the step is latency bound -- one wave's dependent chain, ~1.3 us for
+    // k_step, ~3.1 us for k_step_rows, whose wave does four envs' work -- and one wave per env wins
+    // (config 2, 4,096 envs: 4.19 vs 5.05 us per step); above it the step is issue bound and the
+    // rows layout's 2x fewer instructions per env win (12,288 envs 7.14 vs 7.62 us, 16,384 8.2 vs
+    // 9.25, config 4's 65,536 23.5 vs 28.7; profiles/r05/rows_ab.txt).
+    static constexpr int ROWS_MIN_ENVS = 10240;
+    bool rows_for(int n) const { return step_rows && (rows_forced || n >= ROWS_MIN_ENVS); }
     int wpb_step = 1, wpb_obs = 1;
     int obs_rank_lds = 0;   // small builder: LDS bytes of the largest map's rank table (0: ranks read from L2)
     int n_cu = 0;   // compute units of the device (step_wpb)
@@ -433,6 +444,14 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
 
     eng->lds_step = mdl::step_lds((int)P);
     eng->wpb_step = waves_per_block(eng->lds_step);
+    if (c.step_layout != MDL_STEP_LAYOUT_AUTO && c.step_layout != MDL_STEP_LAYOUT_WAVE &&
+        c.step_layout != MDL_STEP_LAYOUT_ROWS)
+        return fail("unknown step_layout %d", c.step_layout);
+    if (c.step_layout == MDL_STEP_LAYOUT_ROWS && !mdl::step_rows_ok((int)A, (int)P))
+        return fail("step_layout ROWS needs A <= 8 and P <= 64 (A=%d P=%d)", (int)A, (int)P);
+    eng->step_rows = c.step_layout != MDL_STEP_LAYOUT_WAVE && mdl::step_rows_ok((int)A, (int)P);
+    eng->rows_forced = c.step_layout == MDL_STEP_LAYOUT_ROWS;
+    eng->lds_rows = mdl::step_rows_lds((int)P);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) eng->n_cu = prop.multiProcessorCount;
@@ -520,6 +539,12 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
     if (n < 0 || n > eng->p.E) return fail("mdl_step: n=%d out of range", n);
     if (n == 0) return 0;
     DeviceGuard dg(eng->device);
+    if (!env_ids && eng->rows_for(n)) {
+        HIPCHK(mdl::launch_step_rows(eng->p, actions, action_format, n, auto_reset, r_env, r_shaped, done,
+                                     step_wpb(n, eng->n_cu, eng->lds_rows, eng->p.P), eng->lds_rows,
+                                     (hipStream_t)stream));
+        return 0;
+    }
     HIPCHK(mdl::launch_step(eng->p, actions, action_format, env_ids, n, auto_reset, r_env, r_shaped, done,
                             step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, (hipStream_t)stream));
     return 0;
@@ -529,8 +554,10 @@ int mdl_step_floor(MdlEngine* eng, int32_t n, void* stream) {
     if (!eng) return fail("mdl_step_floor: null engine");
     if (n < 1 || n > eng->p.E) return fail("mdl_step_floor: n=%d out of range", n);
     DeviceGuard dg(eng->device);
-    HIPCHK(mdl::launch_step_floor(eng->p, n, step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step,
-                                  (hipStream_t)stream));
+    // the launch shape of a full-batch mdl_step over n envs (the rows grid when that layout is on)
+    const bool rows = eng->rows_for(n);
+    const size_t lds = rows ? eng->lds_rows : eng->lds_step;
+    HIPCHK(mdl::launch_step_floor(eng->p, n, step_wpb(n, eng->n_cu, lds, eng->p.P), lds, (hipStream_t)stream, rows));
     return 0;
 }
 

@@ -1163,6 +1163,8 @@ __global__ __launch_bounds__(256) MDL_STEP_ATTR(1, false) void k_step_obs(const 
     step_body<STALE, 1, false, AU, true>(rob_pre, pkg_pre, pst_pre, es_pre, trk_pre, act_pre, ap, nw, args, oa);
 }
 
+#include "mdl_step_rows.hpp"
+
 // ------------------------------------------------------------- observations
 // Tracker slots staged in LDS for the feature builders (random access by id).
 struct ObsLdsPre {
@@ -1772,14 +1774,52 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
 #undef MDL_STEP_ARGS
 }
 
-hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s) {
+bool step_rows_ok(int A, int P) { return A >= 1 && A <= 8 && P >= 1 && P <= ROW * ROW_NC; }
+size_t step_rows_lds(int P) {
+    const size_t a = reset_lds_bytes(P), b = rows_scratch_bytes();
+    return a > b ? a : b;
+}
+
+hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
+                            float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
+    if (!step_rows_ok(p.A, p.P)) return hipErrorInvalidValue;
+    StepArgs a;
+    a.p = p;
+    a.actions = actions;
+    a.env_ids = nullptr;
+    a.r_out = r;
+    a.sh_out = sh;
+    a.done_out = done;
+    a.fmt = fmt;
+    a.n = n;
+    a.auto_reset = auto_reset;
+    a.wpb = wpb;
+    a.lds_stride = (int)lds;
+    a.K = 1;
+    const int waves = (n + 3) / 4;
+    const dim3 grid(blocks_for(waves, wpb)), block(64 * wpb);
+    const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
+    const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
+#define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a
+    if (p.stale) {
+        if (p.A == 5) hipLaunchKernelGGL((k_step_rows<true, 5>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+        else hipLaunchKernelGGL((k_step_rows<true, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    } else {
+        if (p.A == 5) hipLaunchKernelGGL((k_step_rows<false, 5>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+        else hipLaunchKernelGGL((k_step_rows<false, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    }
+#undef MDL_STEP_ARGS
+    return hipGetLastError();
+}
+
+hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s, bool rows) {
     StepArgs a{};
     a.p = p;
     a.n = n;
     a.wpb = wpb;
     a.lds_stride = (int)lds;
     a.K = 1;
-    const dim3 grid(blocks_for(n, wpb)), block(64 * wpb);
+    const dim3 grid(blocks_for(rows ? (n + 3) / 4 : n, wpb)), block(64 * wpb);
     const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
     hipLaunchKernelGGL(k_step_floor, grid, block, lds * wpb, s, p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk,

@@ -16,8 +16,15 @@ hipError_t launch_reset(const DevParams& p, const int* ids, int n, int wpb, size
 hipError_t launch_tracker_clear(const DevParams& p, const int* ids, int n, hipStream_t s);
 hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int auto_reset,
                        double* r, float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s);
-// the step's launch shape (grid, workgroup, LDS, kernel arguments) with an empty kernel
-hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s);
+// k_step_rows (mdl_step_rows.hpp): a full-batch step with four envs per wavefront, one per 16-lane
+// row; A <= 8, P <= 64 (step_rows_ok).  lds: the per-wave slice (step_rows_lds).
+bool step_rows_ok(int A, int P);
+size_t step_rows_lds(int P);
+hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
+                            float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s);
+// the step's launch shape (grid, workgroup, LDS, kernel arguments) with an empty kernel; rows: the
+// k_step_rows grid (four envs per wave)
+hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s, bool rows = false);
 hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int K,
                              int auto_reset, double* r, float* sh, uint8_t* done, int wpb, size_t lds,
                              hipStream_t s);

@@ -1,0 +1,554 @@
+// mdl_step_rows.hpp -- the step kernel with FOUR ENVS PER WAVEFRONT, one per 16-lane DPP row
+// (included by mdl_kernels.hip after k_step; same reference semantics, env.py:173-316,
+// MAPPO/helper.py:257-369, MAPPO/trainer.py:95-130,211-259).
+//
+// Why: at the configs' A = 5 robots and P = 50 packages, k_step's one wave per env leaves most
+// lanes idle in its serial sections and pays every scalar instruction (kernel prologue, branch and
+// exec-mask handling, readlane chains, loop control) once per env.  The step is issue bound at
+// every measured batch (profiles/r05: ~3 cycles per wave instruction per SIMD, 4096 to 131,072
+// envs).  Here env r of the wave lives on lanes 16r..16r+15: robot a on row lane a (A <= AU <= 8),
+// package j on row lane j & 15 of chunk j >> 4 (P <= 64, four chunks).  Everything an env does is
+// row-local: broadcasts are DPP row_newbcast (one VALU op, no SGPR), minima are four in-row DPP
+// stages, a ballot's row part is one 64-bit vector shift -- and each of those instructions serves
+// four envs.  The scalar instructions are shared by the four envs as well.
+//
+// Scope: full-batch steps (no env_ids), one step per launch, A <= 8, P <= 64; the one-wave-per-env
+// k_step stays for everything else (subset stepping, the fused bench mode, the mailbox and
+// step + observation launches, wider configs).  Results are bit-identical to k_step's
+// (tests/test_gpu_step_rows.py steps both layouts side by side).
+#pragma once
+
+constexpr int ROW = 16;        // lanes per env
+constexpr int ROW_NC = 4;      // package chunks per lane (P <= 64)
+
+// lane J of this lane's row, on every lane of the row (DPP row_newbcast, gfx90a+)
+template <int J>
+__device__ __forceinline__ int row_bcast(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + J, 0xf, 0xf, false);
+}
+template <int J>
+__device__ __forceinline__ float row_bcastf(float v) {
+    return __int_as_float(row_bcast<J>(__float_as_int(v)));
+}
+// this lane's row of a wave mask (bits 16r..16r+15 -> 0..15); rbase = 16r
+__device__ __forceinline__ uint32_t row_bits(uint64_t m, int rbase) { return (uint32_t)(m >> rbase) & 0xffffu; }
+// the union over the four rows of a wave mask
+__device__ __forceinline__ uint32_t rows_union(uint64_t m) { return (uint32_t)((m | (m >> 16) | (m >> 32) | (m >> 48)) & 0xffffull); }
+// minimum over the row, on every lane of the row: xor 1, xor 2, then rotations by 4 and 8
+// (row_ror:n: lane l reads row lane (l - n) & 15)
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t m) {
+    const int id = (int)0xffffffff;
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)m, 0xB1, 0xf, 0xf, false); m = t < m ? t : m;   // quad_perm 1,0,3,2
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)m, 0x4E, 0xf, 0xf, false); m = t < m ? t : m;   // quad_perm 2,3,0,1
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)m, 0x124, 0xf, 0xf, false); m = t < m ? t : m;  // row_ror:4
+    t = (uint32_t)__builtin_amdgcn_update_dpp(id, (int)m, 0x128, 0xf, 0xf, false); m = t < m ? t : m;  // row_ror:8
+    return m;
+}
+__device__ __forceinline__ uint32_t row_or_u32(uint32_t m) {
+    m |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xf, 0xf, false);
+    m |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x4E, 0xf, 0xf, false);
+    m |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x124, 0xf, 0xf, false);
+    m |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x128, 0xf, 0xf, false);
+    return m;
+}
+
+// numpy float32 add.reduce of the row's lanes 0..A-1 (A <= AU), on every lane of the row: the
+// sequential n < 8 branch as a row_shr:1 chain (np_sum_lanes_dpp's argument: lanes A..AU-1 hold
+// +0.0f, no lane holds -0.0f), numpy's 8-partial form when A == 8.
+template <int AU>
+__device__ __forceinline__ float row_np_sum(float v, int A) {
+    static_assert(AU >= 1 && AU <= 8, "row_np_sum: AU <= 8");
+    constexpr int L = AU < 8 ? AU : 7;
+    if (AU == 8 && A == 8) {
+        const float a = v + dppf<0xB1>(v);    // lanes 0, 2, 4, 6: x0+x1, x2+x3, x4+x5, x6+x7
+        const float b = a + dppf<0x4E>(a);    // lanes 0, 4: (x0+x1)+(x2+x3), (x4+x5)+(x6+x7)
+        const float c = b + dppf<0x124>(b);   // lane 4 (row_ror:4 reads lane l - 4): the two halves
+        return 0.0f + row_bcastf<4>(c);
+    }
+    float t = v;
+#pragma unroll
+    for (int i = 1; i < L; i++) t = v + dppf<0x111>(t);   // row_shr:1 (lane 0 of the row reads +0)
+    return row_bcastf<L - 1>(t);
+}
+
+// The carried package's fields a robot needs, gathered through LDS (one 16-byte record per
+// package slot): its state word, env-table target | deadline << 16, tracker target | deadline << 16.
+__device__ __forceinline__ uint32_t tgt_dl(uint64_t v) {
+    return __builtin_amdgcn_perm((uint32_t)(v >> 32), (uint32_t)v, 0x07060302u);
+}
+
+// LDS bytes per wave: the gather records (4 chunks x 64 lanes x 16 B), then the 256 flag bytes;
+// the reset scratch reuses the slice after both are consumed.
+__host__ __device__ constexpr size_t rows_scratch_bytes() { return (size_t)ROW_NC * 64 * 16 + 256; }
+
+// (93 VGPRs, 5 waves per SIMD.  Capping it at 6 waves (79 VGPRs) was 1 % faster on config 4 and 3-6 %
+// slower at 4,096-16,384 envs, at 7 waves 20 % slower: profiles/r05/rows_ab.txt.)
+template <bool STALE, int AU>
+__global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ rob_pre,
+                                                   const uint64_t* __restrict__ pkg_pre,
+                                                   const uint16_t* __restrict__ pst_pre,
+                                                   const u32x4* __restrict__ es_pre,
+                                                   const uint64_t* __restrict__ trk_pre,
+                                                   const uint8_t* __restrict__ act_pre, uint32_t ap, uint32_t nw,
+                                                   StepArgs args) {
+    static_assert(AU >= 1 && AU <= 8, "k_step_rows: A <= 8");
+    extern __shared__ __align__(16) unsigned char smem[];
+    const DevParams& p = args.p;
+    const int A = (int)(ap & 0x7fu), P = (int)((ap >> 7) & 0x7ffu);
+    const int n_ = (int)(nw & 0xffffffu), wpb_ = (int)((nw >> 24) & 31u);
+    GLOBAL const uint32_t* robp = (GLOBAL const uint32_t*)rob_pre;
+    GLOBAL const uint64_t* pkgp = (GLOBAL const uint64_t*)pkg_pre;
+    GLOBAL const uint16_t* pstp = (GLOBAL const uint16_t*)pst_pre;
+    GLOBAL const u32x4* esp = (GLOBAL const u32x4*)es_pre;
+    GLOBAL const uint64_t* trkp = (GLOBAL const uint64_t*)trk_pre;
+    GLOBAL const uint8_t* actp = (GLOBAL const uint8_t*)act_pre;
+
+    const int wave = wave_id();
+    const int lane = lane_id();
+    const int nbp = (int)(ap >> AP_NB_SHIFT);
+    const int w = (nbp ? xcd_slot((int)blockIdx.x, nbp) : (int)blockIdx.x) * wpb_ + wave;
+    const int e0 = 4 * w;   // this wave's envs: e0 .. e0 + 3
+    if (wave >= wpb_ || e0 >= n_) return;
+    const int r = lane >> 4, rl = lane & 15, rbase = lane & 48;
+    const bool live = e0 + r < n_;   // the last wave's rows past n hold no env
+    const bool act = live && rl < A;
+
+    // ---- loads: one round trip, everything independent.  No exec-masked load blocks: every lane
+    // loads (lanes without data read an in-bounds word of env e0 and discard it), so the loads
+    // issue back to back with no branch and no wait between them. ----
+    const uint32_t roff = (uint32_t)(r * A + rl);
+    // (offsets masked to their range -- r * A + rl < 64, r * P + j < 256 -- so the loads take the
+    // scalar-base + 32-bit-offset form instead of a 64-bit address per lane)
+    const uint32_t roff_c = (act ? roff : 0u) & 0x3fu;
+    const uint32_t rv_ld = (robp + (size_t)e0 * A)[roff_c];
+    const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
+    uint64_t pk[ROW_NC], td[ROW_NC];
+    uint32_t ps[ROW_NC], ps_in[ROW_NC], tq[ROW_NC];
+    bool dirty[ROW_NC];
+    GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
+    GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
+    GLOBAL const uint64_t* trke = trkp + (size_t)e0 * P;
+    bool pv[ROW_NC];   // package slot c * 16 + rl of this row exists
+#pragma unroll
+    for (int c = 0; c < ROW_NC; c++) {
+        const int j = c * ROW + rl;
+        pv[c] = live && j < P;
+        const uint32_t o = (pv[c] ? (uint32_t)(r * P + j) : 0u) & 0xffu;
+        pk[c] = pkge[o];
+        ps[c] = pste[o];
+        td[c] = STALE ? trke[o] : 0ull;
+        dirty[c] = false;
+    }
+    const u32x4 esv_ld = (esp + e0)[(uint32_t)(live ? r : 0) & 3u];
+    // cost_sum[k] on row lane k (k <= 8): the move-cost fold of the row's n_cost movers, fetched
+    // by a row-local permute once n_cost is known
+    KargPtr kap = (KargPtr)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                            offsetof(StepKarg, args));
+    const double cst = kap->p.cost_sum[rl < 9 ? rl : 8];
+    __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any use
+    const uint32_t rv = act ? rv_ld : 0u;
+    int araw = act ? (int)(ar_ld & 0xffu) : 0;
+    const u32x4 esv = live ? esv_ld : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int c = 0; c < ROW_NC; c++) {
+        pk[c] = pv[c] ? pk[c] : 0ull;
+        ps[c] = pv[c] ? ps[c] : 0u;
+        td[c] = pv[c] ? td[c] : 0ull;
+        ps_in[c] = ps[c];
+    }
+    const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride;
+    const int T = p.T;
+    unsigned char* slice = smem + (size_t)wave * lds_stride;
+    int mvoff = p.maps[0].mvc_off;
+    int mi = 0;
+    if (nw & NW_MAP) {   // mixed maps: each row's map, its move-validity table by a select chain
+        mi = live ? (int)((GLOBAL const uint8_t*)p.env_map)[e0 + r] : 0;
+#pragma unroll
+        for (int k = 1; k < MAX_MAPS; k++) mvoff = (mi == k) ? p.maps[k].mvc_off : mvoff;
+    }
+    int cell = rob_cell(rv), carry = rob_carry(rv);
+    uint32_t vmask = rob_valid(rv);
+    const int t0 = (int)esv.x;
+    const double tot_cur = __hiloint2double((int)esv.w, (int)esv.z);
+
+    int mv, op;
+    decode_action(araw, fmt, mv, op);
+    mv = act ? mv : MV_S;
+    op = act ? op : 0;
+    uint32_t ps0[ROW_NC];
+#pragma unroll
+    for (int c = 0; c < ROW_NC; c++) {
+        const int j = c * ROW + rl;
+        ps0[c] = ps[c];
+        if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
+            td[c] = pk[c];
+            tq[c] = STALE ? ORD_EPISODE + (uint32_t)j : (uint32_t)j;
+        } else {
+            tq[c] = ps0[c] >> PS_RANK_SHIFT;
+        }
+    }
+
+    // ---- the pre-step carried package of each robot, through LDS (read while the movement runs);
+    // the flag bytes of the package actions (below) are cleared under the same wave barrier ----
+    const int pj = carry - 1;
+    u32x4* grec = (u32x4*)slice;
+    unsigned char* flb = slice + ROW_NC * 64 * 16;   // byte (r, rl * 4 + c) <-> package slot c * 16 + rl of row r
+#pragma unroll
+    for (int c = 0; c < ROW_NC; c++) grec[c * 64 + lane] = u32x4{ps0[c], tgt_dl(pk[c]), tgt_dl(td[c]), 0u};
+    ((uint32_t*)flb)[lane] = 0u;
+    wave_sync();
+    const u32x4 g = grec[((pj >> 4) & 3) * 64 + rbase + (pj & 15)];
+    const uint32_t g_pf = g.x, g_pk = g.y, g_td = g.z;
+
+    // ---- movement (env.py:188-257): as k_step's AU > 0 form, row-local ----
+    const int pcell = cell, pcarry = carry;
+    constexpr uint64_t DTAB = (uint64_t)(0x3ffu & (uint32_t)-256) << 10 | (uint64_t)256 << 20 |
+                              (uint64_t)(0x3ffu & (uint32_t)-1) << 30 | (uint64_t)1 << 40;
+    const int dtab = __builtin_amdgcn_sbfe((int)(uint32_t)(DTAB >> (10 * mv)), 0, 10);
+    const int vok = __builtin_amdgcn_sbfe((int)vmask, mv, 1);
+    const int prop = cell + (int)(lmask(act) & (uint32_t)(dtab & vok));
+    const bool mover = act && prop != cell;
+    const uint64_t movers = ballot(mover);
+    const uint32_t pvm = (uint32_t)(p.movevalid_cell + mvoff)[(uint32_t)prop];
+    uint64_t moved = 0;
+    if (movers) {
+        const int propx = act ? prop : -2, cellx = act ? cell : -3;
+        int pjs[AU], cjs[AU];
+#define MDL_ROWB(J)                          \
+    if constexpr (J < AU) {                  \
+        pjs[J] = row_bcast<J>(propx);        \
+        cjs[J] = row_bcast<J>(cellx);        \
+    }
+        MDL_ROWB(0) MDL_ROWB(1) MDL_ROWB(2) MDL_ROWB(3) MDL_ROWB(4) MDL_ROWB(5) MDL_ROWB(6) MDL_ROWB(7)
+#undef MDL_ROWB
+        uint32_t hit = 0;
+        int occ = -1;
+#pragma unroll
+        for (int j = 0; j < AU; j++) {
+            hit |= pjs[j] == prop ? (1u << j) : 0u;
+            occ = cjs[j] == prop ? j : occ;
+        }
+        const bool blocked = (hit & ((1u << rl) - 1u) & row_bits(movers, rbase)) != 0u;
+        const uint32_t Mbase = lmask(mover && !blocked), Mfree = lmask(occ < 0);
+        moved = ballot((Mbase & Mfree) != 0u);
+        if (ballot((Mbase & ~Mfree) != 0u)) {   // some walk into an occupied cell: resolve the chains
+            const int oln = rbase + (occ & 15);
+            for (int it = 0; it < A; it++) {
+                const uint64_t nm = ballot((Mbase & (Mfree | vbit(moved, oln))) != 0u);
+                if (nm == moved) break;
+                moved = nm;
+            }
+        }
+        if ((moved >> lane) & 1ull) cell = prop;
+    }
+    const int n_cost = (int)__popc(row_bits(moved, rbase));
+
+    // ---- package actions (env.py:259-292) ----
+    // Pick-ups: each picking robot takes the lowest-index waiting package at its cell.  Robots sit on
+    // distinct cells, so their choices are independent of the reference's robot order; per robot
+    // index J, one in-row minimum over the row's package slots answers robot J of all four envs.
+    const bool picker = act && op == 1 && carry == 0;
+    const uint64_t pickers = ballot(picker);
+    int cnew = carry;
+    if (pickers) {
+        const uint32_t pu = rows_union(pickers);
+        int sw[ROW_NC];
+#pragma unroll
+        for (int c = 0; c < ROW_NC; c++) sw[c] = (ps[c] & PS_STATUS) == ST_WAITING ? pk_start(pk[c]) : -2;
+#define MDL_PICK(J)                                                                                  \
+    if constexpr (J < AU) {                                                                          \
+        if (pu & (1u << J)) {                                                                        \
+            const int ci = row_bcast<J>(cell);                                                       \
+            uint32_t k = 127u;                                                                       \
+            _Pragma("unroll") for (int c = ROW_NC - 1; c >= 0; c--) k = sw[c] == ci ? (uint32_t)(c * ROW + rl) : k; \
+            k = row_min_u32(k);                                                                      \
+            cnew = (rl == J && picker && k != 127u) ? (int)k + 1 : cnew;                            \
+        }                                                                                            \
+    }
+        MDL_PICK(0) MDL_PICK(1) MDL_PICK(2) MDL_PICK(3) MDL_PICK(4) MDL_PICK(5) MDL_PICK(6) MDL_PICK(7)
+#undef MDL_PICK
+    }
+    const bool picked = cnew != carry;
+    carry = cnew;
+    // drops: a robot with op 2 carrying a package (its pre-step one: it did not pick) and standing on
+    // that package's target delivers it
+    const int g_tgt = (int)(g_pk & 0xffffu), g_dl = (int)(g_pk >> 16);
+    const bool drop = act && op == 2 && carry != 0 && g_tgt == cell;
+    const uint64_t dmask = ballot(drop), omask = ballot(drop && t0 <= g_dl);
+    // One flag byte per package slot, written by the robot concerned (each robot names at most one
+    // slot, different robots different slots): picked (and now carried), delivered, carried.  The
+    // package lanes read their four slots' bytes in one word: the status changes and, for the
+    // tracker update, the carried ids.
+    constexpr uint32_t F_PICK = 1u, F_DELIV = 2u, F_CARRY = 4u;
+    {
+        const int fs = drop ? pj : carry - 1;
+        const uint32_t fv = picked ? (F_PICK | F_CARRY) : drop ? F_DELIV : F_CARRY;
+        if (act && carry != 0) flb[(rbase << 2) + ((fs & 15) << 2) + (fs >> 4)] = (unsigned char)fv;
+    }
+    carry = drop ? 0 : carry;
+    wave_sync();
+    const uint32_t fw = ((const uint32_t*)flb)[lane];
+#pragma unroll
+    for (int c = 0; c < ROW_NC; c++) {
+        const uint32_t f = fw >> (8 * c);
+        ps[c] = (f & F_PICK) ? ((ps[c] & ~PS_STATUS) | ST_IN_TRANSIT)
+                : (f & F_DELIV) ? ((ps[c] & ~PS_STATUS) | ST_DELIVERED) : ps[c];
+    }
+    // reward: fp64 fold in the reference's order (move costs, then deliveries in robot order)
+    double rr;
+    {
+        const int src = (rbase + n_cost) << 2;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)__double2loint(cst));
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)__double2hiint(cst));
+        rr = __hiloint2double((int)hi, (int)lo);
+    }
+    const uint32_t drow = row_bits(dmask, rbase), orow = row_bits(omask, rbase);
+    if (dmask) {
+        double DR = p.delivery_reward, DL = p.delay_reward;
+        pin(DR);
+        pin(DL);
+        for (uint32_t u = rows_union(dmask); u; u &= u - 1) {
+            const int i = __ffs((int)u) - 1;
+            const double add = ((orow >> i) & 1u) ? DR : DL;
+            rr = ((drow >> i) & 1u) ? rr + add : rr;
+        }
+    }
+    const uint32_t rfl = (n_cost ? RT_MOVE : 0u) | (orow ? RT_ONTIME : 0u) | ((drow & ~orow) ? RT_LATE : 0u);
+    const int t1 = t0 + 1;
+    const double total = tot_cur + rr;
+
+    // ---- terminate (env.py:308-316: every package delivered, or t == T) + spawn (get_state
+    // env.py:133-137) ----
+    bool alld = true;
+    uint64_t spawned = 0;
+#pragma unroll
+    for (int c = 0; c < ROW_NC; c++) {
+        alld = alld && (!pv[c] || (ps[c] & PS_STATUS) == ST_DELIVERED);
+        const bool sp = pv[c] && pk_st(pk[c]) == t1;
+        spawned |= ballot(sp);
+        if (sp) ps[c] = (ps[c] & ~PS_STATUS) | ST_WAITING;
+    }
+    const bool done = live && ((t1 == T) || row_bits(ballot(!alld), rbase) == 0u);
+
+    // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
+    float s_lane;
+    {
+        const uint32_t pf = g_pf;
+        const uint32_t Mact = lmask(act), Mpc0 = lmask(pcarry == 0), Mc0 = lmask(carry == 0);
+        const uint32_t Mpres =
+            Mact & ~Mpc0 & lmask(pcarry <= P) &
+            (STALE ? lmask((pf & PS_PRESENT) != 0)
+                   : lmask((pf & PS_STATUS) == ST_WAITING) | lmask((pf & PS_STATUS) == ST_IN_TRANSIT));
+        const uint32_t Mmov = lmask(pcell != cell), MS = lmask(mv == MV_S);
+        const uint32_t Mop1 = lmask(op == 1), Mop2 = lmask(op == 2);
+        const bool need_can = (Mact & Mop1 & Mpc0 & Mc0) != 0u;
+        int stc[ROW_NC], swv[ROW_NC];
+        uint32_t klo[ROW_NC];   // order key << 10 | row-local slot, or ~0 for no candidate
+        uint64_t anyw = 0;
+#pragma unroll
+        for (int c = 0; c < ROW_NC; c++) {
+            const uint32_t f = ps0[c];
+            const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
+            const bool wv = waiting && pk_st(td[c]) <= t0;
+            stc[c] = pk_start(td[c]);
+            swv[c] = wv ? stc[c] : -1;
+            klo[c] = wv ? (tq[c] << 10) | (uint32_t)(c * ROW + rl) : 0xffffffffu;
+            anyw |= ballot(wv);
+        }
+        uint32_t Midle = 0, Mcan = 0;
+        int best_cell = -1;
+        if (anyw) {
+            // every agent's nearest waiting package (distance << 21 | order key << 10 | slot, the
+            // reference's tie-break), computed for all AU agents of all four rows at once: the
+            // agents that do not need it are masked out by the terms below
+            uint32_t kmin = 0xffffffffu;
+#define MDL_NEAR(J)                                                                                  \
+    if constexpr (J < AU) {                                                                          \
+        const int pa = row_bcast<J>(pcell);                                                          \
+        uint32_t k = 0xffffffffu;                                                                    \
+        _Pragma("unroll") for (int c = 0; c < ROW_NC; c++) {                                         \
+            const uint32_t kc = ((uint32_t)manhattan_sad(pa, stc[c]) << 21) | klo[c];                \
+            k = kc < k ? kc : k;                                                                     \
+        }                                                                                            \
+        k = row_min_u32(k);                                                                          \
+        kmin = rl == J ? k : kmin;                                                                   \
+    }
+            MDL_NEAR(0) MDL_NEAR(1) MDL_NEAR(2) MDL_NEAR(3) MDL_NEAR(4) MDL_NEAR(5) MDL_NEAR(6) MDL_NEAR(7)
+#undef MDL_NEAR
+            const int js = (int)(kmin & 63u);
+            const int sl = (rbase + (js & 15)) << 2;
+            int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);
+#pragma unroll
+            for (int c = 1; c < ROW_NC; c++) {
+                const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
+                bc = (js >> 4) == c ? v : bc;
+            }
+            const bool found = act && kmin != 0xffffffffu;
+            Midle = lmask(found && (kmin >> 21) <= 3u);
+            best_cell = found ? bc : -1;
+            // can-pick-up: a waiting package starts at the agent's (new) cell
+            if (ballot(need_can)) {
+                uint32_t hm = 0;
+#define MDL_CAN(J)                                                                                   \
+    if constexpr (J < AU) {                                                                          \
+        const int ca = row_bcast<J>(cell);                                                           \
+        bool h = false;                                                                              \
+        _Pragma("unroll") for (int c = 0; c < ROW_NC; c++) h = h || swv[c] == ca;                    \
+        hm |= h ? (1u << J) : 0u;                                                                    \
+    }
+                MDL_CAN(0) MDL_CAN(1) MDL_CAN(2) MDL_CAN(3) MDL_CAN(4) MDL_CAN(5) MDL_CAN(6) MDL_CAN(7)
+#undef MDL_CAN
+                hm = row_or_u32(hm);
+                Mcan = ((hm >> rl) & 1u) ? ~0u : 0u;
+            }
+        }
+        float cs[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            cs[k] = p.shaping[k];
+            pin(cs[k]);
+        }
+        const int ptg = (int)(g_td & 0xffffu), pdl = (int)(g_td >> 16);
+        const uint32_t Mtg = lmask(cell == ptg);
+        const uint32_t Mpick = Mpc0 & ~Mc0;
+        const uint32_t Mdeliv = ~Mpc0 & Mc0 & Mpres & Mtg;
+        const float t1v = fmask(Mpick, cs[SH_PICK]) + fmask(Mdeliv, fpick(lmask(t1 <= pdl), cs[SH_ONTIME], cs[SH_LATE]));
+        const uint32_t Mwpick = Mop1 & (~Mpc0 | (Mc0 & ~Mcan));
+        const uint32_t Mwdrop = Mop2 & (Mpc0 | (~Mc0 & Mpres & ~Mtg));
+        const float t2v = fmask(Mwpick, cs[SH_WPICK]) + fmask(Mwdrop, cs[SH_WDROP]);
+        const float t3v = fmask(~MS & ~Mmov, cs[SH_STUCK]);
+        const int tgt = ipick(~Mpc0 & Mpres, ptg, best_cell);
+        const int db = manhattan_sad(pcell, tgt), da = manhattan_sad(cell, tgt);
+        const uint32_t Mt = lmask(tgt >= 0) & Mmov;
+        const float t4v = fmask(Mt & lmask(da < db), cs[SH_CLOSER]) + fmask(Mt & lmask(da > db), cs[SH_AWAY]);
+        const float t5v = fmask(~Mmov & MS & Mpc0 & Midle, cs[SH_IDLE]);
+        float s = t1v;
+        s = s + t2v;
+        s = s + t3v;
+        s = s + t4v;
+        s = s + t5v;
+        s_lane = fmask(Mact, s);
+    }
+    const float shaped = (float)rr + row_np_sum<AU>(s_lane, A);
+
+    // ---- tracker update with the new state (MAPPO/trainer.py:95-130); rows that reset below
+    // update with the reset state instead ----
+    const bool do_rst = done && auto_reset;
+    const uint64_t rst = ballot(do_rst);
+    if (STALE && (ballot(picked) | dmask | spawned)) {
+#pragma unroll
+        for (int c = 0; c < ROW_NC; c++) {
+            const bool ins = pv[c] && !do_rst && (pk_st(pk[c]) == t1) && !(ps[c] & PS_PRESENT);
+            ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
+            td[c] = ins ? pk[c] : td[c];
+            dirty[c] = dirty[c] || ins;
+            const bool carried = ((fw >> (8 * c)) & F_CARRY) != 0u;
+            const uint32_t upd = carried ? (ps[c] | PS_TRANSIT) : (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
+            ps[c] = ((ps[c] & PS_PRESENT) && !do_rst) ? upd : ps[c];
+        }
+    }
+
+    // ---- reset on done (MAPPO/trainer.py:230-235): one row at a time, by the whole wave ----
+    int t_out = do_rst ? 0 : t1;
+    double total_out = do_rst ? 0.0 : total;
+    if (rst) {
+        wave_sync();   // the flag bytes and gather records are consumed (the reset scratch overlays them)
+        for (uint64_t m = rst & 0x0001000100010001ull; m; m &= m - 1) {
+            const int rb = ffs64(m);   // 16 * the resetting row
+            const int er = e0 + (rb >> 4);
+            ResetLds L = reset_carve(slice, P);
+            const int mr = rdl(mi, rb);
+            const MapDesc md = p.maps[mr];
+            const int nc = do_reset(p, er, md, L, false);   // robot a's cell on lane a
+            const int ncr = __builtin_amdgcn_ds_bpermute(rl << 2, nc);
+            const bool mine = rbase == rb;
+            if (mine && act) {
+                cell = ncr;
+                carry = 0;
+                vmask = p.movevalid_cell[(uint32_t)(mvoff + ncr)];
+            }
+            if (STALE) {
+                // every present entry of the row becomes a survivor ranked by its current key
+                uint32_t rk[ROW_NC];
+#pragma unroll
+                for (int c = 0; c < ROW_NC; c++) rk[c] = 0;
+#pragma unroll
+                for (int c2 = 0; c2 < ROW_NC; c2++) {
+                    uint64_t pm = ballot(c2 * ROW + rl < P && (ps[c2] & PS_PRESENT)) & (0xffffull << rb);
+                    while (pm) {
+                        const uint32_t ki = (uint32_t)rdl((int)tq[c2], ffs64(pm));
+                        pm &= pm - 1;
+#pragma unroll
+                        for (int c = 0; c < ROW_NC; c++) rk[c] += ki < tq[c] ? 1u : 0u;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < ROW_NC; c++) {
+                    if (mine) {
+                        if (c * ROW + rl < P && (ps[c] & PS_PRESENT)) {
+                            tq[c] = rk[c];
+                            ps[c] = (ps[c] & PS_FLAGS) | PS_SURVIVOR | (rk[c] << PS_RANK_SHIFT);
+                        } else {
+                            ps[c] &= PS_STATUS;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < ROW_NC; c++) {
+                const int j = c * ROW + rl;
+                if (mine) {
+                    pk[c] = j < P ? L.pk[j] : 0;
+                    ps[c] = (j < P ? (uint32_t)L.pst[j] : 0u) | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
+                    if (STALE) {   // the update with the reset state: inserts at t = 0, nothing carried
+                        const bool ins = (j < P) & (pk_st(pk[c]) == 0) & !(ps[c] & PS_PRESENT);
+                        ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
+                        td[c] = ins ? pk[c] : td[c];
+                        dirty[c] = dirty[c] || ins;
+                        const uint32_t upd = (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
+                        ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
+                    }
+                }
+            }
+            wave_sync();   // L is read by every lane before the next row's reset rewrites it
+        }
+    }
+    vmask = (((moved >> lane) & 1ull) && !do_rst) ? pvm : vmask;
+    asm volatile("" : "+v"(vmask));
+
+    // ---- outputs and write-back (pointers fetched in one late scalar batch, as k_step) ----
+    GLOBAL double* rop = (GLOBAL double*)kap->r_out;
+    GLOBAL float* shp = (GLOBAL float*)kap->sh_out;
+    GLOBAL uint8_t* dnp = (GLOBAL uint8_t*)kap->done_out;
+    GLOBAL uint32_t* robw = (GLOBAL uint32_t*)kap->p.rob;
+    GLOBAL uint16_t* pstw = (GLOBAL uint16_t*)kap->p.pstate;
+    GLOBAL uint64_t* trkw = (GLOBAL uint64_t*)kap->p.trk;
+    GLOBAL uint64_t* pkgw = (GLOBAL uint64_t*)kap->p.pkg;
+    GLOBAL u32x4* esw = (GLOBAL u32x4*)kap->p.es;
+    const int e = e0 + r;
+    if (live && rl == 0) {
+        if (done) {
+            p.ep_total[e] = total;
+            p.ep_len[e] = t1;
+        }
+        if (rop) rop[e] = rr;
+        if (shp) shp[e] = shaped;
+        if (dnp) dnp[e] = done ? 1 : 0;
+        esw[e] = u32x4{(uint32_t)t_out, rfl, (uint32_t)__double2loint(total_out),
+                       (uint32_t)__double2hiint(total_out)};
+    }
+    if (act) (robw + (size_t)e0 * A)[roff] = rob_pack(cell, carry, vmask);
+    const bool rrow = (rst >> lane) & 1ull;   // this row reset: its package table is new
+#pragma unroll
+    for (int c = 0; c < ROW_NC; c++) {
+        const int j = c * ROW + rl;
+        if (live && j < P) {
+            const uint32_t o = (uint32_t)(r * P + j);
+            const size_t eb = (size_t)e0 * P;
+            if (ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
+            if (rrow) (pkgw + eb)[o] = pk[c];
+            if (STALE && dirty[c]) (trkw + eb)[o] = td[c];
+        }
+    }
+}

@@ -32,6 +32,9 @@ MDL_MAX_ROBOTS = 64
 MDL_MAX_PACKAGES = 1024
 MDL_OBS_BUILDER_AUTO = 0
 MDL_OBS_BUILDER_GENERIC = 1
+MDL_STEP_LAYOUT_AUTO = 0
+MDL_STEP_LAYOUT_WAVE = 1
+MDL_STEP_LAYOUT_ROWS = 2
 
 
 class MdlConfig(C.Structure):
@@ -51,6 +54,7 @@ class MdlConfig(C.Structure):
         ("max_robots_state", C.c_int32),
         ("max_packages_state", C.c_int32),
         ("obs_builder", C.c_int32),
+        ("step_layout", C.c_int32),
     ]
 
 

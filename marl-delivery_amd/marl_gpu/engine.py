@@ -33,6 +33,7 @@ TRACKER_MODES = {"fresh": _lib.MDL_TRACKER_FRESH, "mappo": _lib.MDL_TRACKER_MAPP
                  "mappo_stale": _lib.MDL_TRACKER_MAPPO_STALE}
 ACTION_FORMATS = {"int": _lib.MDL_ACTION_TRAINER_INT, "codes": _lib.MDL_ACTION_CODES}
 OBS_BUILDERS = {"auto": _lib.MDL_OBS_BUILDER_AUTO, "generic": _lib.MDL_OBS_BUILDER_GENERIC}
+STEP_LAYOUTS = {"auto": _lib.MDL_STEP_LAYOUT_AUTO, "wave": _lib.MDL_STEP_LAYOUT_WAVE, "rows": _lib.MDL_STEP_LAYOUT_ROWS}
 STATUS_NAMES = ("None", "waiting", "in_transit", "delivered")
 
 
@@ -58,6 +59,10 @@ class BatchedEnv:
                obs_max_time_steps defaults to max_time_steps;
     obs_builder:   "auto" (the small builder where it applies, A <= 8 and P <= 64) or
                "generic" (always the general builder): the same observations either way.
+    step_layout:   "auto" (four envs per wavefront for full-batch steps of >= 10,240 envs where A <= 8
+               and P <= 64),
+               "wave" (one env per wavefront) or "rows" (four per wavefront; an error where it does
+               not apply): the same results either way (MdlConfig.step_layout).
     After construction every env holds the constructor's layout draw; call
     ``reset()`` for the first episode, as the reference trainers do.
     """
@@ -67,7 +72,8 @@ class BatchedEnv:
                  seed: int = 2025, seeds: Sequence[int] | None = None, env_map: Sequence[int] | None = None,
                  tracker: str = "mappo", shaping="mappo", max_other_robots: int | None = None,
                  max_packages_obs: int = 5, max_robots_state: int = 100, max_packages_state: int = 100,
-                 obs_max_time_steps: int | None = None, obs_builder: str = "auto", device=None):
+                 obs_max_time_steps: int | None = None, obs_builder: str = "auto", step_layout: str = "auto",
+                 device=None):
         if not torch.cuda.is_available():
             raise RuntimeError("marl_gpu.BatchedEnv needs a ROCm GPU (no CPU fallback)")
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
@@ -97,6 +103,10 @@ class BatchedEnv:
         cfg.max_other_robots, cfg.max_packages_obs = self.MO, self.MP
         cfg.max_robots_state, cfg.max_packages_state = self.MR, self.MPs
         cfg.obs_builder = OBS_BUILDERS[obs_builder]
+        cfg.step_layout = STEP_LAYOUTS[step_layout]
+        # whether a full-batch step runs four envs per wavefront (the engine's rule: MdlEngine::rows_for)
+        self.step_rows = step_layout != "wave" and self.A <= 8 and self.P <= 64 and \
+            (step_layout == "rows" or self.E >= 10240)
         self.cfg = cfg
         flat = np.ascontiguousarray(np.concatenate([g.reshape(-1) for g in self.grids]).astype(np.uint8))
         hw = np.array([[g.shape[0], g.shape[1]] for g in self.grids], np.int32).reshape(-1)

@@ -87,13 +87,18 @@ def _check_obs(o, d, k, map_steps, pre="", big=None):
         np.testing.assert_array_equal(o["critic_map"], d["cmap"][j], err_msg=f"{pre} cmap step {k}")
 
 
+@pytest.mark.parametrize("layout", ["wave", "rows"])
 @pytest.mark.parametrize("tag", ["mappo", "mappo_map2", "mappo_syn64"])
-def test_mappo_rollout_golden(tag):
+def test_mappo_rollout_golden(tag, layout):
+    """The reference's MAPPO rollout, through both step layouts (rows: four envs per wavefront,
+    where A <= 8 and P <= 64)."""
     mg = _mg()
     d = npz(f"rollout_{tag}.npz")
     m = meta(d)
     E, A, P, T = m["E"], m["A"], m["P"], m["T"]
-    kw = dict(seed=m["seed"], tracker="mappo", shaping="mappo")
+    if layout == "rows" and (A > 8 or P > 64):
+        pytest.skip("the rows layout needs A <= 8 and P <= 64")
+    kw = dict(seed=m["seed"], tracker="mappo", shaping="mappo", step_layout=layout)
     env = mg.BatchedEnv(grid(m["map"]), E, A, P, T, max_other_robots=m["MO"], max_packages_obs=m["MP"],
                         max_robots_state=m["MR"], max_packages_state=m["MPs"], **kw)
     envq = mg.BatchedEnv(grid(m["map"]), E, A, P, T, max_other_robots=m["MO"], max_packages_obs=m["MP"],
@@ -269,10 +274,11 @@ def test_notebook_kat():
 
 
 # --------------------------------------------------- GPU vs oracle, larger
-def _oracle_compare(mapname, E, A, P, T, seed, steps, tracker, check_every=10, rng_seed=0):
+def _oracle_compare(mapname, E, A, P, T, seed, steps, tracker, check_every=10, rng_seed=0, layout="auto"):
     mg = _mg()
     g = grid(mapname) if isinstance(mapname, str) else mapname
-    env = mg.BatchedEnv(g, E, A, P, T, seed=seed, tracker=tracker, shaping="mappo", max_packages_obs=5)
+    env = mg.BatchedEnv(g, E, A, P, T, seed=seed, tracker=tracker, shaping="mappo", max_packages_obs=5,
+                        step_layout=layout)
     env.reset()
     ob = O.OracleBatch(E, g, A, P, T, seed_base=seed, clear_on_reset=(tracker == "fresh"))
     rs = np.random.RandomState(rng_seed)
@@ -295,9 +301,18 @@ def _oracle_compare(mapname, E, A, P, T, seed, steps, tracker, check_every=10, r
     env.close()
 
 
+@pytest.mark.parametrize("layout", ["wave", "rows"])
 @pytest.mark.parametrize("tracker", ["mappo", "fresh"])
-def test_vs_oracle_map1(tracker):
-    _oracle_compare("map1.txt", 64, 5, 50, 60, 1000, 200, tracker)
+def test_vs_oracle_map1(tracker, layout):
+    _oracle_compare("map1.txt", 64, 5, 50, 60, 1000, 200, tracker, layout=layout)
+
+
+@pytest.mark.parametrize("mapname,A,P,T", [("map1.txt", 1, 20, 40), ("map1.txt", 3, 50, 40), ("map2.txt", 8, 60, 40),
+                                           ("map1.txt", 7, 30, 40), ("map3.txt", 5, 64, 30)])
+def test_vs_oracle_rows_layout(mapname, A, P, T):
+    """k_step_rows (four envs per wavefront) against the oracle: A < 5, A = 5, A = 8 (numpy's
+    8-partial sum), P up to 64; 37 envs leave the last wave's rows partly empty."""
+    _oracle_compare(mapname, 37, A, P, T, 700 + A, 90, "mappo", layout="rows")
 
 
 @pytest.mark.parametrize("mapname,A,P,T", [("map1.txt", 1, 20, 40), ("map1.txt", 3, 50, 40), ("map2.txt", 8, 60, 40),

@@ -1,0 +1,128 @@
+"""The four-envs-per-wavefront step (k_step_rows, MdlConfig.step_layout "rows") against the
+one-env-per-wavefront step (k_step, "wave"): same seeds, same actions, every output and the whole
+engine state (save_state: robots, packages, statuses, tracker, per-env scalars and reward-term bits,
+RNG words, episode records) bit for bit after every step -- across auto-resets, in both tracker
+modes, both action formats, A < 5 / A = 5 / A = 8 (numpy's 8-partial sum), P from 1 to 64 (one to
+four package chunks per lane), env counts that leave the last wave's rows empty, and mixed maps.
+The oracle and golden-fixture tests run this kernel too (test_gpu_parity.py: test_vs_oracle_rows_layout,
+the "rows" cases of test_vs_oracle_map1 and test_mappo_rollout_golden); the default layout ("auto")
+picks it for full-batch steps of >= 10,240 envs (test_rows_auto_threshold)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from golden_io import grid  # noqa: E402
+
+
+def _mg():
+    import marl_gpu
+    return marl_gpu
+
+
+def _pair(maps, E, A, P, T, **kw):
+    mg = _mg()
+    a = mg.BatchedEnv(maps, E, A, P, T, step_layout="wave", **kw)
+    b = mg.BatchedEnv(maps, E, A, P, T, step_layout="rows", **kw)
+    a.reset()
+    b.reset()
+    return a, b
+
+
+def _run(a, b, steps, seed, fmt="int", check_every=1):
+    E, A = a.E, a.A
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    hi = 15 if fmt == "int" else 64
+    n_done = 0
+    for k in range(steps):
+        acts = torch.randint(0, hi, (E, A), dtype=torch.uint8, device="cuda", generator=gen)
+        r1, s1, d1 = a.step(acts, action_format=fmt)
+        r2, s2, d2 = b.step(acts, action_format=fmt)
+        torch.cuda.synchronize()
+        assert torch.equal(r1, r2), f"r_env differs at step {k}"
+        assert torch.equal(s1.view(torch.int32), s2.view(torch.int32)), f"r_shaped differs at step {k}"
+        assert torch.equal(d1, d2), f"done differs at step {k}"
+        n_done += int(d1.sum())
+        if (k + 1) % check_every == 0 or k == steps - 1:
+            sa, sb = a.save_state(), b.save_state()
+            if not np.array_equal(sa, sb):
+                bad = np.nonzero(sa != sb)[0]
+                raise AssertionError(f"state differs after step {k}: {bad.size} bytes from offset {bad[0]}")
+    return n_done
+
+
+@pytest.mark.parametrize("tracker", ["mappo", "fresh"])
+def test_rows_equals_wave_config2(tracker):
+    a, b = _pair(grid("map1.txt"), 1024, 5, 50, 40, seed=11, tracker=tracker)
+    assert _run(a, b, 130, seed=1, check_every=10) > 0   # three auto-resets of every env
+
+
+@pytest.mark.parametrize("A,P,E,T", [(5, 64, 257, 25), (5, 1, 130, 12), (8, 40, 301, 30), (3, 17, 66, 20),
+                                     (1, 33, 99, 15), (7, 48, 203, 35), (8, 64, 128, 18), (2, 16, 5, 10)])
+def test_rows_equals_wave_shapes(A, P, E, T):
+    a, b = _pair(grid("map2.txt"), E, A, P, T, seed=3 + A + P, tracker="mappo")
+    _run(a, b, 2 * T + 7, seed=A * 100 + P)
+
+
+def test_rows_equals_wave_codes_fresh():
+    a, b = _pair(grid("map3.txt"), 200, 5, 30, 22, seed=5, tracker="fresh")
+    _run(a, b, 50, seed=4, fmt="codes")
+
+
+def test_rows_equals_wave_mixed_maps():
+    maps = [grid(f"map{i}.txt") for i in range(1, 6)]
+    E = 403
+    env_map = np.repeat(np.arange(5), [81, 80, 81, 80, 81])
+    a, b = _pair(maps, E, 5, 50, 30, seed=21, tracker="mappo", env_map=env_map)
+    _run(a, b, 70, seed=8, check_every=7)
+
+
+def test_rows_no_auto_reset_and_subset():
+    """auto_reset off (done envs keep stepping) and a subset step in between (one wave per env)."""
+    a, b = _pair(grid("map1.txt"), 300, 5, 50, 9, seed=2, tracker="mappo")
+    gen = torch.Generator(device="cuda").manual_seed(6)
+    ids = torch.arange(1, 300, 3, dtype=torch.int32, device="cuda")
+    for k in range(30):
+        acts = torch.randint(0, 15, (300, 5), dtype=torch.uint8, device="cuda", generator=gen)
+        if k % 4 == 3:
+            sub = acts[: ids.numel()].contiguous()
+            a.step(sub, env_ids=ids)
+            b.step(sub, env_ids=ids)
+        else:
+            r1, s1, d1 = a.step(acts, auto_reset=k < 20)
+            r2, s2, d2 = b.step(acts, auto_reset=k < 20)
+            assert torch.equal(r1, r2) and torch.equal(s1.view(torch.int32), s2.view(torch.int32))
+            assert torch.equal(d1, d2)
+        torch.cuda.synchronize()
+        assert np.array_equal(a.save_state(), b.save_state()), k
+
+
+def test_rows_layout_refused_where_it_does_not_apply():
+    mg = _mg()
+    with pytest.raises(RuntimeError):
+        mg.BatchedEnv(grid("map1.txt"), 8, 9, 20, 10, step_layout="rows")
+    with pytest.raises(RuntimeError):
+        mg.BatchedEnv(grid("map1.txt"), 8, 5, 65, 10, step_layout="rows")
+    env = mg.BatchedEnv(grid("map1.txt"), 8, 9, 20, 10)   # auto: one wave per env there
+    env.reset()
+    env.step(torch.zeros((8, 9), dtype=torch.uint8, device="cuda"))
+
+
+def test_rows_auto_threshold():
+    """auto: one wave per env below 10,240 envs, four per wave from there on; same results."""
+    mg = _mg()
+    small = mg.BatchedEnv(grid("map1.txt"), 10239, 5, 50, 30, seed=1)
+    big = mg.BatchedEnv(grid("map1.txt"), 10240, 5, 50, 30, seed=1)
+    assert not small.step_rows and big.step_rows
+    ref = mg.BatchedEnv(grid("map1.txt"), 10240, 5, 50, 30, seed=1, step_layout="wave")
+    for e in (big, ref):
+        e.reset()
+    gen = torch.Generator(device="cuda").manual_seed(12)
+    for k in range(40):
+        acts = torch.randint(0, 15, (10240, 5), dtype=torch.uint8, device="cuda", generator=gen)
+        r1, s1, d1 = big.step(acts)
+        r2, s2, d2 = ref.step(acts)
+        assert torch.equal(r1, r2) and torch.equal(s1.view(torch.int32), s2.view(torch.int32)) and torch.equal(d1, d2)
+    torch.cuda.synchronize()
+    assert np.array_equal(big.save_state(), ref.save_state())

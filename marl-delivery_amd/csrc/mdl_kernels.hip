@@ -1774,9 +1774,11 @@ static void launch_step_t(const DevParams& p, const uint8_t* actions, int fmt, c
 #undef MDL_STEP_ARGS
 }
 
-bool step_rows_ok(int A, int P) { return A >= 1 && A <= 8 && P >= 1 && P <= ROW * ROW_NC; }
+// P <= 64 (four chunks per lane).  Eight chunks (P <= 128) were built and measured slower than
+// k_step at P = 100 (16,384 envs 14.2 vs 10.6 us, 65,536 39.7 vs 33.9: profiles/r05/rows_ab.txt)
+bool step_rows_ok(int A, int P) { return A >= 1 && A <= 8 && P >= 1 && P <= ROW * 4; }
 size_t step_rows_lds(int P) {
-    const size_t a = reset_lds_bytes(P), b = rows_scratch_bytes();
+    const size_t a = reset_lds_bytes(P), b = rows_scratch_bytes(4);
     return a > b ? a : b;
 }
 
@@ -1801,13 +1803,14 @@ hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt,
     const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a
-    if (p.stale) {
-        if (p.A == 5) hipLaunchKernelGGL((k_step_rows<true, 5>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
-        else hipLaunchKernelGGL((k_step_rows<true, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
-    } else {
-        if (p.A == 5) hipLaunchKernelGGL((k_step_rows<false, 5>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
-        else hipLaunchKernelGGL((k_step_rows<false, 8>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
-    }
+#define MDL_ROWS(ST, NC)                                                                                  \
+    do {                                                                                                  \
+        if (p.A == 5) hipLaunchKernelGGL((k_step_rows<ST, 5, NC>), grid, block, lds * wpb, s, MDL_STEP_ARGS);   \
+        else hipLaunchKernelGGL((k_step_rows<ST, 8, NC>), grid, block, lds * wpb, s, MDL_STEP_ARGS);      \
+    } while (0)
+    if (p.stale) MDL_ROWS(true, 4);
+    else MDL_ROWS(false, 4);
+#undef MDL_ROWS
 #undef MDL_STEP_ARGS
     return hipGetLastError();
 }

@@ -7,7 +7,8 @@
 // exec-mask handling, readlane chains, loop control) once per env.  The step is issue bound at
 // every measured batch (profiles/r05: ~3 cycles per wave instruction per SIMD, 4096 to 131,072
 // envs).  Here env r of the wave lives on lanes 16r..16r+15: robot a on row lane a (A <= AU <= 8),
-// package j on row lane j & 15 of chunk j >> 4 (P <= 64, four chunks).  Everything an env does is
+// package j on row lane j & 15 of chunk j >> 4 (NC = 4 chunks, P <= 64; the code is written for
+// NC = 8 too, which measured slower than k_step at P = 100 and is not instantiated).  Everything an env does is
 // row-local: broadcasts are DPP row_newbcast (one VALU op, no SGPR), minima are four in-row DPP
 // stages, a ballot's row part is one 64-bit vector shift -- and each of those instructions serves
 // four envs.  The scalar instructions are shared by the four envs as well.
@@ -19,7 +20,7 @@
 #pragma once
 
 constexpr int ROW = 16;        // lanes per env
-constexpr int ROW_NC = 4;      // package chunks per lane (P <= 64)
+// package chunks per lane: NC = 4 (P <= 64) or 8 (P <= 128), a template parameter of the kernel
 
 // lane J of this lane's row, on every lane of the row (DPP row_newbcast, gfx90a+)
 template <int J>
@@ -80,11 +81,15 @@ __device__ __forceinline__ uint32_t tgt_dl(uint64_t v) {
 
 // LDS bytes per wave: the gather records (4 chunks x 64 lanes x 16 B), then the 256 flag bytes;
 // the reset scratch reuses the slice after both are consumed.
-__host__ __device__ constexpr size_t rows_scratch_bytes() { return (size_t)ROW_NC * 64 * 16 + 256; }
+__host__ __device__ constexpr size_t rows_scratch_bytes(int NC) { return (size_t)NC * 64 * 16 + 64 * (size_t)NC; }
+// one flag byte per package slot, a lane's NC slots in one load
+template <int NC> struct FlagWord;
+template <> struct FlagWord<4> { typedef uint32_t T; };
+template <> struct FlagWord<8> { typedef uint64_t T; };
 
 // (93 VGPRs, 5 waves per SIMD.  Capping it at 6 waves (79 VGPRs) was 1 % faster on config 4 and 3-6 %
 // slower at 4,096-16,384 envs, at 7 waves 20 % slower: profiles/r05/rows_ab.txt.)
-template <bool STALE, int AU>
+template <bool STALE, int AU, int NC>
 __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ rob_pre,
                                                    const uint64_t* __restrict__ pkg_pre,
                                                    const uint16_t* __restrict__ pst_pre,
@@ -93,6 +98,8 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
                                                    const uint8_t* __restrict__ act_pre, uint32_t ap, uint32_t nw,
                                                    StepArgs args) {
     static_assert(AU >= 1 && AU <= 8, "k_step_rows: A <= 8");
+    static_assert(NC == 4 || NC == 8, "k_step_rows: P <= 64 or P <= 128");
+    constexpr uint32_t NONE = 255u;   // no package slot (slots < 16 * NC <= 128)
     extern __shared__ __align__(16) unsigned char smem[];
     const DevParams& p = args.p;
     const int A = (int)(ap & 0x7fu), P = (int)((ap >> 7) & 0x7ffu);
@@ -118,40 +125,40 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     // loads (lanes without data read an in-bounds word of env e0 and discard it), so the loads
     // issue back to back with no branch and no wait between them. ----
     const uint32_t roff = (uint32_t)(r * A + rl);
-    // (offsets masked to their range -- r * A + rl < 64, r * P + j < 256 -- so the loads take the
+    // (offsets masked to their range -- r * A + rl < 64, r * P + j < 512 -- so the loads take the
     // scalar-base + 32-bit-offset form instead of a 64-bit address per lane)
     const uint32_t roff_c = (act ? roff : 0u) & 0x3fu;
     const uint32_t rv_ld = (robp + (size_t)e0 * A)[roff_c];
     const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
-    uint64_t pk[ROW_NC], td[ROW_NC];
-    uint32_t ps[ROW_NC], ps_in[ROW_NC], tq[ROW_NC];
-    bool dirty[ROW_NC];
+    uint64_t pk[NC], td[NC];
+    uint32_t ps[NC], ps_in[NC], tq[NC];
+    bool dirty[NC];
     GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
     GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
     GLOBAL const uint64_t* trke = trkp + (size_t)e0 * P;
-    bool pv[ROW_NC];   // package slot c * 16 + rl of this row exists
+    bool pv[NC];   // package slot c * 16 + rl of this row exists
 #pragma unroll
-    for (int c = 0; c < ROW_NC; c++) {
+    for (int c = 0; c < NC; c++) {
         const int j = c * ROW + rl;
         pv[c] = live && j < P;
-        const uint32_t o = (pv[c] ? (uint32_t)(r * P + j) : 0u) & 0xffu;
+        const uint32_t o = (pv[c] ? (uint32_t)(r * P + j) : 0u) & 0x1ffu;
         pk[c] = pkge[o];
         ps[c] = pste[o];
         td[c] = STALE ? trke[o] : 0ull;
         dirty[c] = false;
     }
     const u32x4 esv_ld = (esp + e0)[(uint32_t)(live ? r : 0) & 3u];
-    // cost_sum[k] on row lane k (k <= 8): the move-cost fold of the row's n_cost movers, fetched
+    // cost_fold[k] on row lane k (k <= A <= 8): the move-cost fold of the row's n_cost movers, fetched
     // by a row-local permute once n_cost is known
     KargPtr kap = (KargPtr)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
                             offsetof(StepKarg, args));
-    const double cst = kap->p.cost_sum[rl < 9 ? rl : 8];
+    const double cst = kap->p.cost_fold[rl];
     __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any use
     const uint32_t rv = act ? rv_ld : 0u;
     int araw = act ? (int)(ar_ld & 0xffu) : 0;
     const u32x4 esv = live ? esv_ld : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int c = 0; c < ROW_NC; c++) {
+    for (int c = 0; c < NC; c++) {
         pk[c] = pv[c] ? pk[c] : 0ull;
         ps[c] = pv[c] ? ps[c] : 0u;
         td[c] = pv[c] ? td[c] : 0ull;
@@ -176,9 +183,9 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     decode_action(araw, fmt, mv, op);
     mv = act ? mv : MV_S;
     op = act ? op : 0;
-    uint32_t ps0[ROW_NC];
+    uint32_t ps0[NC];
 #pragma unroll
-    for (int c = 0; c < ROW_NC; c++) {
+    for (int c = 0; c < NC; c++) {
         const int j = c * ROW + rl;
         ps0[c] = ps[c];
         if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
@@ -193,12 +200,13 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     // the flag bytes of the package actions (below) are cleared under the same wave barrier ----
     const int pj = carry - 1;
     u32x4* grec = (u32x4*)slice;
-    unsigned char* flb = slice + ROW_NC * 64 * 16;   // byte (r, rl * 4 + c) <-> package slot c * 16 + rl of row r
+    unsigned char* flb = slice + NC * 64 * 16;   // byte (r, rl * NC + c) <-> package slot c * 16 + rl of row r
+    typedef typename FlagWord<NC>::T FW;
 #pragma unroll
-    for (int c = 0; c < ROW_NC; c++) grec[c * 64 + lane] = u32x4{ps0[c], tgt_dl(pk[c]), tgt_dl(td[c]), 0u};
-    ((uint32_t*)flb)[lane] = 0u;
+    for (int c = 0; c < NC; c++) grec[c * 64 + lane] = u32x4{ps0[c], tgt_dl(pk[c]), tgt_dl(td[c]), 0u};
+    ((FW*)flb)[lane] = 0;
     wave_sync();
-    const u32x4 g = grec[((pj >> 4) & 3) * 64 + rbase + (pj & 15)];
+    const u32x4 g = grec[((pj >> 4) & (NC - 1)) * 64 + rbase + (pj & 15)];
     const uint32_t g_pf = g.x, g_pk = g.y, g_td = g.z;
 
     // ---- movement (env.py:188-257): as k_step's AU > 0 form, row-local ----
@@ -253,17 +261,17 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     int cnew = carry;
     if (pickers) {
         const uint32_t pu = rows_union(pickers);
-        int sw[ROW_NC];
+        int sw[NC];
 #pragma unroll
-        for (int c = 0; c < ROW_NC; c++) sw[c] = (ps[c] & PS_STATUS) == ST_WAITING ? pk_start(pk[c]) : -2;
+        for (int c = 0; c < NC; c++) sw[c] = (ps[c] & PS_STATUS) == ST_WAITING ? pk_start(pk[c]) : -2;
 #define MDL_PICK(J)                                                                                  \
     if constexpr (J < AU) {                                                                          \
         if (pu & (1u << J)) {                                                                        \
             const int ci = row_bcast<J>(cell);                                                       \
-            uint32_t k = 127u;                                                                       \
-            _Pragma("unroll") for (int c = ROW_NC - 1; c >= 0; c--) k = sw[c] == ci ? (uint32_t)(c * ROW + rl) : k; \
+            uint32_t k = NONE;                                                                           \
+            _Pragma("unroll") for (int c = NC - 1; c >= 0; c--) k = sw[c] == ci ? (uint32_t)(c * ROW + rl) : k; \
             k = row_min_u32(k);                                                                      \
-            cnew = (rl == J && picker && k != 127u) ? (int)k + 1 : cnew;                            \
+            cnew = (rl == J && picker && k != NONE) ? (int)k + 1 : cnew;                             \
         }                                                                                            \
     }
         MDL_PICK(0) MDL_PICK(1) MDL_PICK(2) MDL_PICK(3) MDL_PICK(4) MDL_PICK(5) MDL_PICK(6) MDL_PICK(7)
@@ -278,20 +286,20 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     const uint64_t dmask = ballot(drop), omask = ballot(drop && t0 <= g_dl);
     // One flag byte per package slot, written by the robot concerned (each robot names at most one
     // slot, different robots different slots): picked (and now carried), delivered, carried.  The
-    // package lanes read their four slots' bytes in one word: the status changes and, for the
+    // package lanes read their NC slots' bytes in one word: the status changes and, for the
     // tracker update, the carried ids.
     constexpr uint32_t F_PICK = 1u, F_DELIV = 2u, F_CARRY = 4u;
     {
         const int fs = drop ? pj : carry - 1;
         const uint32_t fv = picked ? (F_PICK | F_CARRY) : drop ? F_DELIV : F_CARRY;
-        if (act && carry != 0) flb[(rbase << 2) + ((fs & 15) << 2) + (fs >> 4)] = (unsigned char)fv;
+        if (act && carry != 0) flb[(rbase + (fs & 15)) * NC + (fs >> 4)] = (unsigned char)fv;
     }
     carry = drop ? 0 : carry;
     wave_sync();
-    const uint32_t fw = ((const uint32_t*)flb)[lane];
+    const FW fw = ((const FW*)flb)[lane];
 #pragma unroll
-    for (int c = 0; c < ROW_NC; c++) {
-        const uint32_t f = fw >> (8 * c);
+    for (int c = 0; c < NC; c++) {
+        const uint32_t f = (uint32_t)(fw >> (8 * c));
         ps[c] = (f & F_PICK) ? ((ps[c] & ~PS_STATUS) | ST_IN_TRANSIT)
                 : (f & F_DELIV) ? ((ps[c] & ~PS_STATUS) | ST_DELIVERED) : ps[c];
     }
@@ -323,7 +331,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     bool alld = true;
     uint64_t spawned = 0;
 #pragma unroll
-    for (int c = 0; c < ROW_NC; c++) {
+    for (int c = 0; c < NC; c++) {
         alld = alld && (!pv[c] || (ps[c] & PS_STATUS) == ST_DELIVERED);
         const bool sp = pv[c] && pk_st(pk[c]) == t1;
         spawned |= ballot(sp);
@@ -343,11 +351,11 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         const uint32_t Mmov = lmask(pcell != cell), MS = lmask(mv == MV_S);
         const uint32_t Mop1 = lmask(op == 1), Mop2 = lmask(op == 2);
         const bool need_can = (Mact & Mop1 & Mpc0 & Mc0) != 0u;
-        int stc[ROW_NC], swv[ROW_NC];
-        uint32_t klo[ROW_NC];   // order key << 10 | row-local slot, or ~0 for no candidate
+        int stc[NC], swv[NC];
+        uint32_t klo[NC];   // order key << 10 | row-local slot, or ~0 for no candidate
         uint64_t anyw = 0;
 #pragma unroll
-        for (int c = 0; c < ROW_NC; c++) {
+        for (int c = 0; c < NC; c++) {
             const uint32_t f = ps0[c];
             const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
             const bool wv = waiting && pk_st(td[c]) <= t0;
@@ -367,7 +375,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     if constexpr (J < AU) {                                                                          \
         const int pa = row_bcast<J>(pcell);                                                          \
         uint32_t k = 0xffffffffu;                                                                    \
-        _Pragma("unroll") for (int c = 0; c < ROW_NC; c++) {                                         \
+        _Pragma("unroll") for (int c = 0; c < NC; c++) {                                         \
             const uint32_t kc = ((uint32_t)manhattan_sad(pa, stc[c]) << 21) | klo[c];                \
             k = kc < k ? kc : k;                                                                     \
         }                                                                                            \
@@ -376,11 +384,11 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     }
             MDL_NEAR(0) MDL_NEAR(1) MDL_NEAR(2) MDL_NEAR(3) MDL_NEAR(4) MDL_NEAR(5) MDL_NEAR(6) MDL_NEAR(7)
 #undef MDL_NEAR
-            const int js = (int)(kmin & 63u);
+            const int js = (int)(kmin & 127u);
             const int sl = (rbase + (js & 15)) << 2;
             int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);
 #pragma unroll
-            for (int c = 1; c < ROW_NC; c++) {
+            for (int c = 1; c < NC; c++) {
                 const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
                 bc = (js >> 4) == c ? v : bc;
             }
@@ -394,7 +402,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     if constexpr (J < AU) {                                                                          \
         const int ca = row_bcast<J>(cell);                                                           \
         bool h = false;                                                                              \
-        _Pragma("unroll") for (int c = 0; c < ROW_NC; c++) h = h || swv[c] == ca;                    \
+        _Pragma("unroll") for (int c = 0; c < NC; c++) h = h || swv[c] == ca;                    \
         hm |= h ? (1u << J) : 0u;                                                                    \
     }
                 MDL_CAN(0) MDL_CAN(1) MDL_CAN(2) MDL_CAN(3) MDL_CAN(4) MDL_CAN(5) MDL_CAN(6) MDL_CAN(7)
@@ -438,12 +446,12 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     const uint64_t rst = ballot(do_rst);
     if (STALE && (ballot(picked) | dmask | spawned)) {
 #pragma unroll
-        for (int c = 0; c < ROW_NC; c++) {
+        for (int c = 0; c < NC; c++) {
             const bool ins = pv[c] && !do_rst && (pk_st(pk[c]) == t1) && !(ps[c] & PS_PRESENT);
             ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
             td[c] = ins ? pk[c] : td[c];
             dirty[c] = dirty[c] || ins;
-            const bool carried = ((fw >> (8 * c)) & F_CARRY) != 0u;
+            const bool carried = ((uint32_t)(fw >> (8 * c)) & F_CARRY) != 0u;
             const uint32_t upd = carried ? (ps[c] | PS_TRANSIT) : (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
             ps[c] = ((ps[c] & PS_PRESENT) && !do_rst) ? upd : ps[c];
         }
@@ -470,21 +478,21 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
             }
             if (STALE) {
                 // every present entry of the row becomes a survivor ranked by its current key
-                uint32_t rk[ROW_NC];
+                uint32_t rk[NC];
 #pragma unroll
-                for (int c = 0; c < ROW_NC; c++) rk[c] = 0;
+                for (int c = 0; c < NC; c++) rk[c] = 0;
 #pragma unroll
-                for (int c2 = 0; c2 < ROW_NC; c2++) {
+                for (int c2 = 0; c2 < NC; c2++) {
                     uint64_t pm = ballot(c2 * ROW + rl < P && (ps[c2] & PS_PRESENT)) & (0xffffull << rb);
                     while (pm) {
                         const uint32_t ki = (uint32_t)rdl((int)tq[c2], ffs64(pm));
                         pm &= pm - 1;
 #pragma unroll
-                        for (int c = 0; c < ROW_NC; c++) rk[c] += ki < tq[c] ? 1u : 0u;
+                        for (int c = 0; c < NC; c++) rk[c] += ki < tq[c] ? 1u : 0u;
                     }
                 }
 #pragma unroll
-                for (int c = 0; c < ROW_NC; c++) {
+                for (int c = 0; c < NC; c++) {
                     if (mine) {
                         if (c * ROW + rl < P && (ps[c] & PS_PRESENT)) {
                             tq[c] = rk[c];
@@ -496,7 +504,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
                 }
             }
 #pragma unroll
-            for (int c = 0; c < ROW_NC; c++) {
+            for (int c = 0; c < NC; c++) {
                 const int j = c * ROW + rl;
                 if (mine) {
                     pk[c] = j < P ? L.pk[j] : 0;
@@ -541,7 +549,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     if (act) (robw + (size_t)e0 * A)[roff] = rob_pack(cell, carry, vmask);
     const bool rrow = (rst >> lane) & 1ull;   // this row reset: its package table is new
 #pragma unroll
-    for (int c = 0; c < ROW_NC; c++) {
+    for (int c = 0; c < NC; c++) {
         const int j = c * ROW + rl;
         if (live && j < P) {
             const uint32_t o = (uint32_t)(r * P + j);

@@ -21,7 +21,7 @@ PMC = {"c2": ("k_step<", ":4096,5,50,map1.txt:k_step<:0"),
        "c3": ("k_step_obs", ":16384,5,50,map1.txt:k_step_obs:1"),
        "c5": ("k_step<", ":16384,16,100,synthetic64.txt:k_step<:0")}
 # full-size launches of bench.py --config 4 / --config 5 (scripts/profile_r05_full.sh): FETCH_SIZE / WRITE_SIZE only
-PMC_FULL = {"c4": ("k_step<", ":65536,5,50," + "+".join(f"map{i}.txt" for i in range(1, 6)) + ":k_step<:0"),
+PMC_FULL = {"c4": ("k_step_rows<", ":65536,5,50," + "+".join(f"map{i}.txt" for i in range(1, 6)) + ":k_step_rows<:0"),
             "c5full": ("k_step<", ":131072,16,100,synthetic64.txt:k_step<:0")}
 
 

@@ -16,6 +16,6 @@ pmc() {   # dir log counter rx -- bench args
 E="--cpu-seconds 0 --no-graph --graph-only --fused-k 0 --no-floor --steps 100 --warmup 10"
 for k in fetch write; do
   case $k in fetch) C=FETCH_SIZE ;; write) C=WRITE_SIZE ;; esac
-  pmc c4/$k c4_$k $C "k_step[<(]" $E --config 4
+  pmc c4/$k c4_$k $C "k_step_rows" $E --config 4   # config 4 runs four envs per wavefront (k_step_rows)
   pmc c5full/$k c5full_$k $C "k_step[<(]" $E --config 5
 done

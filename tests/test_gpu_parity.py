@@ -308,10 +308,11 @@ def test_vs_oracle_map1(tracker, layout):
 
 
 @pytest.mark.parametrize("mapname,A,P,T", [("map1.txt", 1, 20, 40), ("map1.txt", 3, 50, 40), ("map2.txt", 8, 60, 40),
-                                           ("map1.txt", 7, 30, 40), ("map3.txt", 5, 64, 30)])
+                                           ("map1.txt", 7, 30, 40), ("map3.txt", 5, 64, 30),
+                                           ("synthetic64.txt", 5, 64, 40)])
 def test_vs_oracle_rows_layout(mapname, A, P, T):
     """k_step_rows (four envs per wavefront) against the oracle: A < 5, A = 5, A = 8 (numpy's
-    8-partial sum), P up to 64; 37 envs leave the last wave's rows partly empty."""
+    8-partial sum), P up to 64, the 64x64 map; 37 envs leave the last wave's rows partly empty."""
     _oracle_compare(mapname, 37, A, P, T, 700 + A, 90, "mappo", layout="rows")
 
 

@@ -2,8 +2,8 @@
 one-env-per-wavefront step (k_step, "wave"): same seeds, same actions, every output and the whole
 engine state (save_state: robots, packages, statuses, tracker, per-env scalars and reward-term bits,
 RNG words, episode records) bit for bit after every step -- across auto-resets, in both tracker
-modes, both action formats, A < 5 / A = 5 / A = 8 (numpy's 8-partial sum), P from 1 to 64 (one to
-four package chunks per lane), env counts that leave the last wave's rows empty, and mixed maps.
+modes, both action formats, A < 5 / A = 5 / A = 8 (numpy's 8-partial sum), P from 1 to 64 (four or eight package chunks per lane), env counts that leave the last
+wave's rows empty, and mixed maps.
 The oracle and golden-fixture tests run this kernel too (test_gpu_parity.py: test_vs_oracle_rows_layout,
 the "rows" cases of test_vs_oracle_map1 and test_mappo_rollout_golden); the default layout ("auto")
 picks it for full-batch steps of >= 10,240 envs (test_rows_auto_threshold)."""
@@ -65,6 +65,13 @@ def test_rows_equals_wave_shapes(A, P, E, T):
     _run(a, b, 2 * T + 7, seed=A * 100 + P)
 
 
+@pytest.mark.parametrize("mapname,A,P,E,T", [("synthetic64.txt", 5, 64, 66, 40), ("synthetic64.txt", 8, 50, 50, 30)])
+def test_rows_equals_wave_large_map(mapname, A, P, E, T):
+    """The 64x64 map (cells up to 63 | 63 << 8, distances up to 126)."""
+    a, b = _pair(grid(mapname), E, A, P, T, seed=40 + A + P, tracker="mappo")
+    _run(a, b, 2 * T + 5, seed=A * 7 + P, check_every=5)
+
+
 def test_rows_equals_wave_codes_fresh():
     a, b = _pair(grid("map3.txt"), 200, 5, 30, 22, seed=5, tracker="fresh")
     _run(a, b, 50, seed=4, fmt="codes")
@@ -104,6 +111,8 @@ def test_rows_layout_refused_where_it_does_not_apply():
         mg.BatchedEnv(grid("map1.txt"), 8, 9, 20, 10, step_layout="rows")
     with pytest.raises(RuntimeError):
         mg.BatchedEnv(grid("map1.txt"), 8, 5, 65, 10, step_layout="rows")
+    with pytest.raises(RuntimeError):
+        mg.BatchedEnv(grid("map2.txt"), 8, 16, 50, 10, step_layout="rows")
     env = mg.BatchedEnv(grid("map1.txt"), 8, 9, 20, 10)   # auto: one wave per env there
     env.reset()
     env.step(torch.zeros((8, 9), dtype=torch.uint8, device="cuda"))

@@ -14,12 +14,12 @@ d = json.loads(open('$O/$t.json').read().strip().splitlines()[-1])
 print('$t', 'us/step %.3f' % (d['ms_per_step'] * 1e3))"
 }
 for rep in $(seq 1 ${REPS:-2}); do
-  run wave_c4_$rep $R/marl-delivery_amd/marl_gpu/libmdl.so wave --config 4 --steps 300 --warmup 30 || exit 1
+  [ "${NOWAVE:-0}" = 1 ] || run wave_c4_$rep $R/marl-delivery_amd/marl_gpu/libmdl.so wave --config 4 --steps 300 --warmup 30 || exit 1
   for V in ${VARIANTS:-w5 w6 w7}; do
     run ${V}_c4_$rep $R/marl-delivery_amd/build/ab/libmdl_$V.so rows --config 4 --steps 300 --warmup 30 || exit 1
   done
   for E in ${ENVS:-4096 8192 12288 16384}; do
-    run wave_e${E}_$rep $R/marl-delivery_amd/marl_gpu/libmdl.so wave --envs $E --steps 1000 --warmup 100 || exit 1
+    [ "${NOWAVE:-0}" = 1 ] || run wave_e${E}_$rep $R/marl-delivery_amd/marl_gpu/libmdl.so wave --envs $E --steps 1000 --warmup 100 || exit 1
     for V in ${VARIANTS:-w5 w6 w7}; do
       run ${V}_e${E}_$rep $R/marl-delivery_amd/build/ab/libmdl_$V.so rows --envs $E --steps 1000 --warmup 100 || exit 1
     done

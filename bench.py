@@ -530,7 +530,8 @@ def main(argv=None):
                        "obs_dims": ({"actor_vec": env.actor_vec_dim, "critic_vec": env.critic_vec_dim,
                                      "obs_bytes_per_env_step": obs_bytes_env} if obs_cfg else None),
                        "parallelism": f"env-shard x{world}",
-                       "step_layout": "rows (4 envs per wavefront)" if env.step_rows else "wave (1 env per wavefront)"},
+                       "step_layout": ("rows (4 envs per wavefront)" if env.step_rows and not obs_cfg
+                                       else "wave (1 env per wavefront)")},
             "gpu_event_ms_per_step": gpu_ms / K,
             "eager": None if wall_eager is None else {"value": total_agent_steps / wall_eager,
                                                        "ms_per_step": wall_eager / K * 1e3},

@@ -50,10 +50,11 @@ def trim_pmc(src_dir, dst_file, kern):
 def main():
     os.makedirs(DST, exist_ok=True)
     stats = {"driver": "driver_command_kernel_stats.csv", "trace": "config2_bench2000_kernel_stats.csv",
-             "c3trace": "config3_bench_kernel_stats.csv", "c5trace": "config5_bench_kernel_stats.csv"}
+             "c3trace": "config3_bench_kernel_stats.csv", "c4trace": "config4_bench_kernel_stats.csv",
+             "c5trace": "config5_bench_kernel_stats.csv"}
     for d, name in stats.items():
         shutil.copy(one(f"{d}/**/run_kernel_stats.csv"), os.path.join(DST, name))
-    for name in ("driver_bench", "trace_bench", "c3_bench", "c5_bench"):
+    for name in ("driver_bench", "trace_bench", "c3_bench", "c4_bench", "c5_bench"):
         shutil.copy(os.path.join(SRC, name + ".json"), os.path.join(DST, name + ".json"))
     summary = []
     for cfg, (kern, _) in PMC.items():
@@ -79,7 +80,7 @@ def main():
         for r in csv.DictReader(open(os.path.join(DST, f))):
             if r["Name"].startswith("void mdl::") or r["Name"].startswith("mdl::"):
                 summary.append(f"{f}: {r['Name'][:70]} calls {r['Calls']} avg {float(r['AverageNs']) / 1e3:.3f} us")
-    for name in ("driver_bench", "trace_bench", "c3_bench", "c5_bench"):
+    for name in ("driver_bench", "trace_bench", "c3_bench", "c4_bench", "c5_bench"):
         d = json.loads(open(os.path.join(DST, name + ".json")).read().strip().splitlines()[-1])
         summary.append(f"{name}: value {d['value']:.4e} ms_per_step {d['ms_per_step']:.6f} kernel_us "
                        f"{d['roofline']['kernel_us']:.3f} frac {d['roofline']['frac']:.4f} "

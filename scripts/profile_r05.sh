@@ -24,6 +24,7 @@ pmc() {   # dir log counters... -- bench args
 run driver_bench 300 rocprofv3 --kernel-trace --stats -d $O/driver -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5
 run trace_bench 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 --graph-only --fused-k 0 --steps 2000 --warmup 20
 run c3_bench 300 rocprofv3 --kernel-trace --stats -d $O/c3trace -o run --output-format csv -- python3 $R/bench.py --config 3 --cpu-seconds 0 --graph-only --steps 300 --warmup 20
+run c4_bench 300 rocprofv3 --kernel-trace --stats -d $O/c4trace -o run --output-format csv -- python3 $R/bench.py --config 4 --cpu-seconds 0 --graph-only --fused-k 0 --steps 300 --warmup 20
 run c5_bench 300 rocprofv3 --kernel-trace --stats -d $O/c5trace -o run --output-format csv -- python3 $R/bench.py --config 5 --cpu-seconds 0 --graph-only --fused-k 0 --steps 300 --warmup 20
 E="--cpu-seconds 0 --no-graph --graph-only --fused-k 0 --no-floor --steps 200 --warmup 20"
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"

@@ -252,6 +252,30 @@ def test_step_kernels_fit_eight_waves_without_scratch(tmp_path):
     assert not spill, spill
 
 
+@pytest.mark.skipif(not os.path.exists(f"{LLVM_BIN}/llvm-readelf"), reason="ROCm LLVM tools absent")
+def test_rows_step_kernels_have_no_scratch(tmp_path):
+    """k_step_rows (four envs per wavefront, csrc/mdl_step_rows.hpp): one instantiation per tracker mode
+    and robot specialisation (A == 5, A <= 8), four package chunks; no spill to scratch, the A == 5
+    form within 104 VGPRs (5 waves per SIMD, the occupancy profiles/r05/rows_ab.txt was measured at),
+    the A <= 8 form within 128 (4 waves)."""
+    from marl_gpu import _lib
+    res = _kernel_resources(_lib.LIB_PATH, tmp_path)
+    rows = [n for n in res if "k_step_rows" in n]
+    assert len(rows) == 4, rows
+    for n in rows:
+        assert res[n]["private_segment_fixed_size"] == 0, (n, res[n])
+        assert res[n]["vgpr_count"] <= (104 if "ILi5ELi4E" in n else 128), (n, res[n])
+
+
+def test_bench_step_layout_flag():
+    """bench.py --step-layout reaches BatchedEnv (MdlConfig.step_layout); auto is the default."""
+    bench = _bench_module()
+    assert bench.parse([]).step_layout == "auto"
+    assert bench.parse(["--config", "4", "--step-layout", "wave"]).step_layout == "wave"
+    with pytest.raises(SystemExit):
+        bench.parse(["--step-layout", "diagonal"])
+
+
 _PROFILING_SWITCHES = ["MDL_EXP_NOWAIT", "MDL_EXP_NOTUPLES", "MDL_EXP_NOLDS", "MDL_ABLATE=1", "MDL_STAMPS"]
 
 

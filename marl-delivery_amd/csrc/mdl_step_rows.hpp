@@ -147,7 +147,11 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         td[c] = STALE ? trke[o] : 0ull;
         dirty[c] = false;
     }
-    const u32x4 esv_ld = (esp + e0)[(uint32_t)(live ? r : 0) & 3u];
+    // the env record's clock and total (its reward-term word is only written): two loads, so no
+    // register of an unused component is recycled under a load still in flight (a forced wait)
+    const uint32_t erow = (uint32_t)(live ? r : 0) & 3u;
+    const uint32_t t_ld = ((GLOBAL const uint32_t*)(esp + e0))[4u * erow];
+    const uint64_t tot_ld = ((GLOBAL const uint64_t*)(esp + e0))[2u * erow + 1u];
     // cost_fold[k] on row lane k (k <= A <= 8): the move-cost fold of the row's n_cost movers, fetched
     // by a row-local permute once n_cost is known
     KargPtr kap = (KargPtr)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
@@ -156,12 +160,17 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any use
     const uint32_t rv = act ? rv_ld : 0u;
     int araw = act ? (int)(ar_ld & 0xffu) : 0;
-    const u32x4 esv = live ? esv_ld : u32x4{0u, 0u, 0u, 0u};
+    const uint32_t t_rec = live ? t_ld : 0u;
+    const uint64_t tot_rec = live ? tot_ld : 0ull;
+    // Slots without a package (j >= P, or a row past n) hold sentinels that fail every test by
+    // themselves, so only the loads and the stores test the slot's existence: status delivered (the
+    // all-delivered test passes over them; not waiting, not present), start time 0xffff (never
+    // spawned or inserted: t < 0xffff), start cell 0xffff (no cell of a map of at most 255 rows).
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        pk[c] = pv[c] ? pk[c] : 0ull;
-        ps[c] = pv[c] ? ps[c] : 0u;
-        td[c] = pv[c] ? td[c] : 0ull;
+        pk[c] = pv[c] ? pk[c] : ~0ull;
+        ps[c] = pv[c] ? ps[c] : (uint32_t)ST_DELIVERED;
+        td[c] = pv[c] ? td[c] : ~0ull;
         ps_in[c] = ps[c];
     }
     const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride;
@@ -170,14 +179,14 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     int mvoff = p.maps[0].mvc_off;
     int mi = 0;
     if (nw & NW_MAP) {   // mixed maps: each row's map, its move-validity table by a select chain
-        mi = live ? (int)((GLOBAL const uint8_t*)p.env_map)[e0 + r] : 0;
+        mi = (int)((GLOBAL const uint8_t*)p.env_map)[e0 + (live ? r : 0)];
 #pragma unroll
         for (int k = 1; k < MAX_MAPS; k++) mvoff = (mi == k) ? p.maps[k].mvc_off : mvoff;
     }
     int cell = rob_cell(rv), carry = rob_carry(rv);
     uint32_t vmask = rob_valid(rv);
-    const int t0 = (int)esv.x;
-    const double tot_cur = __hiloint2double((int)esv.w, (int)esv.z);
+    const int t0 = (int)t_rec;
+    const double tot_cur = __hiloint2double((int)(uint32_t)(tot_rec >> 32), (int)(uint32_t)tot_rec);
 
     int mv, op;
     decode_action(araw, fmt, mv, op);
@@ -288,20 +297,22 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     // slot, different robots different slots): picked (and now carried), delivered, carried.  The
     // package lanes read their NC slots' bytes in one word: the status changes and, for the
     // tracker update, the carried ids.
-    constexpr uint32_t F_PICK = 1u, F_DELIV = 2u, F_CARRY = 4u;
+    // byte = the slot's new status (bits 0-1) | F_CHG (status changed) | F_CARRY (carried after the step)
+    constexpr uint32_t F_CHG = 8u, F_CARRY = 4u;
     {
         const int fs = drop ? pj : carry - 1;
-        const uint32_t fv = picked ? (F_PICK | F_CARRY) : drop ? F_DELIV : F_CARRY;
+        const uint32_t fv = picked ? (F_CHG | F_CARRY | (uint32_t)ST_IN_TRANSIT)
+                            : drop ? (F_CHG | (uint32_t)ST_DELIVERED) : F_CARRY;
         if (act && carry != 0) flb[(rbase + (fs & 15)) * NC + (fs >> 4)] = (unsigned char)fv;
     }
     carry = drop ? 0 : carry;
     wave_sync();
     const FW fw = ((const FW*)flb)[lane];
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
+    for (int c = 0; c < NC; c++) {   // bit arithmetic, no branch: unchanged slots' bytes have status bits 0
         const uint32_t f = (uint32_t)(fw >> (8 * c));
-        ps[c] = (f & F_PICK) ? ((ps[c] & ~PS_STATUS) | ST_IN_TRANSIT)
-                : (f & F_DELIV) ? ((ps[c] & ~PS_STATUS) | ST_DELIVERED) : ps[c];
+        const uint32_t clr = (0u - ((f >> 3) & 1u)) & PS_STATUS;
+        ps[c] = (ps[c] & ~clr) | (f & PS_STATUS);
     }
     // reward: fp64 fold in the reference's order (move costs, then deliveries in robot order)
     double rr;
@@ -328,16 +339,18 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
 
     // ---- terminate (env.py:308-316: every package delivered, or t == T) + spawn (get_state
     // env.py:133-137) ----
-    bool alld = true;
+    uint32_t undel = 0;   // nonzero: some slot of this lane is not delivered (sentinel slots are)
     uint64_t spawned = 0;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        alld = alld && (!pv[c] || (ps[c] & PS_STATUS) == ST_DELIVERED);
-        const bool sp = pv[c] && pk_st(pk[c]) == t1;
+        undel |= (ps[c] & PS_STATUS) ^ (uint32_t)ST_DELIVERED;
+        const bool sp = pk_st(pk[c]) == t1;
         spawned |= ballot(sp);
-        if (sp) ps[c] = (ps[c] & ~PS_STATUS) | ST_WAITING;
+        ps[c] = sp ? ((ps[c] & ~PS_STATUS) | ST_WAITING) : ps[c];
     }
-    const bool done = live && ((t1 == T) || row_bits(ballot(!alld), rbase) == 0u);
+    // (no short-circuit: a ballot under a divergent branch costs exec juggling)
+    const uint32_t alldel = lmask(row_bits(ballot(undel != 0u), rbase) == 0u);
+    const bool done = (lmask(live) & (lmask(t1 == T) | alldel)) != 0u;
 
     // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
     float s_lane;
@@ -447,13 +460,15 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     if (STALE && (ballot(picked) | dmask | spawned)) {
 #pragma unroll
         for (int c = 0; c < NC; c++) {
-            const bool ins = pv[c] && !do_rst && (pk_st(pk[c]) == t1) && !(ps[c] & PS_PRESENT);
+            const bool ins = !do_rst && (pk_st(pk[c]) == t1) && !(ps[c] & PS_PRESENT);
             ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
             td[c] = ins ? pk[c] : td[c];
             dirty[c] = dirty[c] || ins;
-            const bool carried = ((uint32_t)(fw >> (8 * c)) & F_CARRY) != 0u;
-            const uint32_t upd = carried ? (ps[c] | PS_TRANSIT) : (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
-            ps[c] = ((ps[c] & PS_PRESENT) && !do_rst) ? upd : ps[c];
+            // present entries: carried -> in transit; in transit and not carried -> deleted (status only)
+            const uint32_t m_p = lmask((ps[c] & PS_PRESENT) != 0u && !do_rst);
+            const uint32_t m_c = lmask(((uint32_t)(fw >> (8 * c)) & F_CARRY) != 0u);
+            const uint32_t m_t = lmask((ps[c] & PS_TRANSIT) != 0u);
+            ps[c] = (ps[c] | (PS_TRANSIT & m_c & m_p)) & (PS_STATUS | ~(m_p & ~m_c & m_t));
         }
     }
 

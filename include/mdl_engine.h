@@ -69,7 +69,7 @@ typedef struct {
 
 /* MdlConfig.step_layout.  ROWS: a full-batch mdl_step (env_ids NULL) runs four envs per wavefront,
  * one per 16-lane row (A <= 8, P <= 64; mdl_create fails otherwise).  WAVE: one env per wavefront
- * always.  AUTO: ROWS where it applies and the batch has at least 10,240 envs (where it is the
+ * always.  AUTO: ROWS where it applies and the batch has at least 7,168 envs (where it is the
  * faster of the two on MI355X), WAVE otherwise.  Subset steps (env_ids), mdl_step_fused,
  * mdl_step_obs and the mailbox step always use one wave per env.  Every layout produces the same
  * state and outputs; WAVE / ROWS exist so tests can compare the two on one configuration. */

@@ -122,12 +122,12 @@ struct MdlEngine {
     bool rows_forced = false; // MDL_STEP_LAYOUT_ROWS: at every batch size
     size_t lds_rows = 0;
     // Whether a full-batch step over n envs runs four envs per wavefront.  AUTO: from ROWS_MIN_ENVS
-    // envs on.  Below that the step is latency bound -- one wave's dependent chain, ~1.3 us for
-    // k_step, ~3.1 us for k_step_rows, whose wave does four envs' work -- and one wave per env wins
-    // (config 2, 4,096 envs: 4.19 vs 5.05 us per step); above it the step is issue bound and the
-    // rows layout's 2x fewer instructions per env win (12,288 envs 7.14 vs 7.62 us, 16,384 8.2 vs
-    // 9.25, config 4's 65,536 23.5 vs 28.7; profiles/r05/rows_ab.txt).
-    static constexpr int ROWS_MIN_ENVS = 10240;
+    // envs on.  Below that the step is latency bound -- one wave's dependent chain is longer for
+    // k_step_rows, whose wave does four envs' work -- and one wave per env wins (4,096 envs: 4.19
+    // vs 4.44 us per step, 6,144: 4.99 vs 5.32); above it the step is issue bound and the rows
+    // layout's ~2x fewer instructions per env win (8,192 envs 5.83 vs 5.45 us, 10,240 6.75 vs 6.38,
+    // config 4's 65,536 28.7 vs 21.1; profiles/r05/rows_ab.txt).
+    static constexpr int ROWS_MIN_ENVS = 7168;
     bool rows_for(int n) const { return step_rows && (rows_forced || n >= ROWS_MIN_ENVS); }
     int wpb_step = 1, wpb_obs = 1;
     int obs_rank_lds = 0;   // small builder: LDS bytes of the largest map's rank table (0: ranks read from L2)

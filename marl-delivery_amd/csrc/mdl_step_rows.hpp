@@ -205,6 +205,55 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         }
     }
 
+    // ---- the shaped reward's pre-step part (MAPPO/helper.py:257-369): every agent's nearest waiting
+    // package of tracker_prev, from its pre-step cell -- nothing here depends on this step's
+    // movement or package actions, so these in-row minima are issued first and run alongside
+    // those dependent chains.  Computed for all AU agents of all four rows (the terms below mask
+    // the agents that do not need it); key = distance << 21 | order key << 10 | slot (the
+    // reference's tie-break). ----
+    int stc[NC], swv[NC];
+    uint32_t klo[NC];   // order key << 10 | row-local slot, or ~0 for no candidate
+    uint64_t anyw = 0;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const uint32_t f = ps0[c];
+        const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
+        const bool wv = waiting && pk_st(td[c]) <= t0;
+        stc[c] = pk_start(td[c]);
+        swv[c] = wv ? stc[c] : -1;
+        klo[c] = wv ? (tq[c] << 10) | (uint32_t)(c * ROW + rl) : 0xffffffffu;
+        anyw |= ballot(wv);
+    }
+    uint32_t Midle = 0;
+    int best_cell = -1;
+    if (anyw) {
+        uint32_t kmin = 0xffffffffu;
+#define MDL_NEAR(J)                                                                                  \
+    if constexpr (J < AU) {                                                                          \
+        const int pa = row_bcast<J>(cell);                                                           \
+        uint32_t k = 0xffffffffu;                                                                    \
+        _Pragma("unroll") for (int c = 0; c < NC; c++) {                                             \
+            const uint32_t kc = ((uint32_t)manhattan_sad(pa, stc[c]) << 21) | klo[c];                \
+            k = kc < k ? kc : k;                                                                     \
+        }                                                                                            \
+        k = row_min_u32(k);                                                                          \
+        kmin = rl == J ? k : kmin;                                                                   \
+    }
+        MDL_NEAR(0) MDL_NEAR(1) MDL_NEAR(2) MDL_NEAR(3) MDL_NEAR(4) MDL_NEAR(5) MDL_NEAR(6) MDL_NEAR(7)
+#undef MDL_NEAR
+        const int js = (int)(kmin & 127u);
+        const int sl = (rbase + (js & 15)) << 2;
+        int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);
+#pragma unroll
+        for (int c = 1; c < NC; c++) {
+            const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
+            bc = (js >> 4) == c ? v : bc;
+        }
+        const bool found = act && kmin != 0xffffffffu;
+        Midle = lmask(found && (kmin >> 21) <= 3u);
+        best_cell = found ? bc : -1;
+    }
+
     // ---- the pre-step carried package of each robot, through LDS (read while the movement runs);
     // the flag bytes of the package actions (below) are cleared under the same wave barrier ----
     const int pj = carry - 1;
@@ -364,50 +413,8 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         const uint32_t Mmov = lmask(pcell != cell), MS = lmask(mv == MV_S);
         const uint32_t Mop1 = lmask(op == 1), Mop2 = lmask(op == 2);
         const bool need_can = (Mact & Mop1 & Mpc0 & Mc0) != 0u;
-        int stc[NC], swv[NC];
-        uint32_t klo[NC];   // order key << 10 | row-local slot, or ~0 for no candidate
-        uint64_t anyw = 0;
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            const uint32_t f = ps0[c];
-            const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
-            const bool wv = waiting && pk_st(td[c]) <= t0;
-            stc[c] = pk_start(td[c]);
-            swv[c] = wv ? stc[c] : -1;
-            klo[c] = wv ? (tq[c] << 10) | (uint32_t)(c * ROW + rl) : 0xffffffffu;
-            anyw |= ballot(wv);
-        }
-        uint32_t Midle = 0, Mcan = 0;
-        int best_cell = -1;
+        uint32_t Mcan = 0;
         if (anyw) {
-            // every agent's nearest waiting package (distance << 21 | order key << 10 | slot, the
-            // reference's tie-break), computed for all AU agents of all four rows at once: the
-            // agents that do not need it are masked out by the terms below
-            uint32_t kmin = 0xffffffffu;
-#define MDL_NEAR(J)                                                                                  \
-    if constexpr (J < AU) {                                                                          \
-        const int pa = row_bcast<J>(pcell);                                                          \
-        uint32_t k = 0xffffffffu;                                                                    \
-        _Pragma("unroll") for (int c = 0; c < NC; c++) {                                         \
-            const uint32_t kc = ((uint32_t)manhattan_sad(pa, stc[c]) << 21) | klo[c];                \
-            k = kc < k ? kc : k;                                                                     \
-        }                                                                                            \
-        k = row_min_u32(k);                                                                          \
-        kmin = rl == J ? k : kmin;                                                                   \
-    }
-            MDL_NEAR(0) MDL_NEAR(1) MDL_NEAR(2) MDL_NEAR(3) MDL_NEAR(4) MDL_NEAR(5) MDL_NEAR(6) MDL_NEAR(7)
-#undef MDL_NEAR
-            const int js = (int)(kmin & 127u);
-            const int sl = (rbase + (js & 15)) << 2;
-            int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);
-#pragma unroll
-            for (int c = 1; c < NC; c++) {
-                const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
-                bc = (js >> 4) == c ? v : bc;
-            }
-            const bool found = act && kmin != 0xffffffffu;
-            Midle = lmask(found && (kmin >> 21) <= 3u);
-            best_cell = found ? bc : -1;
             // can-pick-up: a waiting package starts at the agent's (new) cell
             if (ballot(need_can)) {
                 uint32_t hm = 0;
@@ -415,7 +422,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     if constexpr (J < AU) {                                                                          \
         const int ca = row_bcast<J>(cell);                                                           \
         bool h = false;                                                                              \
-        _Pragma("unroll") for (int c = 0; c < NC; c++) h = h || swv[c] == ca;                    \
+        _Pragma("unroll") for (int c = 0; c < NC; c++) h = h | (swv[c] == ca);                   \
         hm |= h ? (1u << J) : 0u;                                                                    \
     }
                 MDL_CAN(0) MDL_CAN(1) MDL_CAN(2) MDL_CAN(3) MDL_CAN(4) MDL_CAN(5) MDL_CAN(6) MDL_CAN(7)
@@ -522,8 +529,8 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
             for (int c = 0; c < NC; c++) {
                 const int j = c * ROW + rl;
                 if (mine) {
-                    pk[c] = j < P ? L.pk[j] : 0;
-                    ps[c] = (j < P ? (uint32_t)L.pst[j] : 0u) | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
+                    pk[c] = j < P ? L.pk[j] : ~0ull;   // (the sentinels again past P)
+                    ps[c] = j < P ? ((uint32_t)L.pst[j] | (STALE ? (ps[c] & ~PS_STATUS) : 0u)) : (uint32_t)ST_DELIVERED;
                     if (STALE) {   // the update with the reset state: inserts at t = 0, nothing carried
                         const bool ins = (j < P) & (pk_st(pk[c]) == 0) & !(ps[c] & PS_PRESENT);
                         ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
@@ -549,29 +556,30 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     GLOBAL uint64_t* trkw = (GLOBAL uint64_t*)kap->p.trk;
     GLOBAL uint64_t* pkgw = (GLOBAL uint64_t*)kap->p.pkg;
     GLOBAL u32x4* esw = (GLOBAL u32x4*)kap->p.es;
-    const int e = e0 + r;
+    // every store: a scalar row base (env e0's) + a 32-bit lane offset, one flat predicate each
+    const uint32_t er = (uint32_t)r & 3u;
     if (live && rl == 0) {
-        if (done) {
-            p.ep_total[e] = total;
-            p.ep_len[e] = t1;
-        }
-        if (rop) rop[e] = rr;
-        if (shp) shp[e] = shaped;
-        if (dnp) dnp[e] = done ? 1 : 0;
-        esw[e] = u32x4{(uint32_t)t_out, rfl, (uint32_t)__double2loint(total_out),
-                       (uint32_t)__double2hiint(total_out)};
+        if (rop) (rop + e0)[er] = rr;
+        if (shp) (shp + e0)[er] = shaped;
+        if (dnp) (dnp + e0)[er] = done ? 1 : 0;
+        (esw + e0)[er] = u32x4{(uint32_t)t_out, rfl, (uint32_t)__double2loint(total_out),
+                               (uint32_t)__double2hiint(total_out)};
+    }
+    if (live && rl == 0 && done) {
+        ((GLOBAL double*)p.ep_total + e0)[er] = total;
+        ((GLOBAL int32_t*)p.ep_len + e0)[er] = t1;
     }
     if (act) (robw + (size_t)e0 * A)[roff] = rob_pack(cell, carry, vmask);
     const bool rrow = (rst >> lane) & 1ull;   // this row reset: its package table is new
+    const size_t eb = (size_t)e0 * P;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
         const int j = c * ROW + rl;
-        if (live && j < P) {
-            const uint32_t o = (uint32_t)(r * P + j);
-            const size_t eb = (size_t)e0 * P;
-            if (ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
-            if (rrow) (pkgw + eb)[o] = pk[c];
-            if (STALE && dirty[c]) (trkw + eb)[o] = td[c];
-        }
+        const uint32_t o = (uint32_t)(r * P + j) & 0x1ffu;
+        // a sentinel slot's state word never changes and it is never inserted, so only the reset
+        // row's table store tests the slot's existence
+        if (ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
+        if (rrow && j < P) (pkgw + eb)[o] = pk[c];
+        if (STALE && dirty[c]) (trkw + eb)[o] = td[c];
     }
 }

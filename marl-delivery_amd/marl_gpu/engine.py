@@ -59,7 +59,7 @@ class BatchedEnv:
                obs_max_time_steps defaults to max_time_steps;
     obs_builder:   "auto" (the small builder where it applies, A <= 8 and P <= 64) or
                "generic" (always the general builder): the same observations either way.
-    step_layout:   "auto" (four envs per wavefront for full-batch steps of >= 10,240 envs where A <= 8
+    step_layout:   "auto" (four envs per wavefront for full-batch steps of >= 7,168 envs where A <= 8
                and P <= 64),
                "wave" (one env per wavefront) or "rows" (four per wavefront; an error where it does
                not apply): the same results either way (MdlConfig.step_layout).
@@ -106,7 +106,7 @@ class BatchedEnv:
         cfg.step_layout = STEP_LAYOUTS[step_layout]
         # whether a full-batch step runs four envs per wavefront (the engine's rule: MdlEngine::rows_for)
         self.step_rows = step_layout != "wave" and self.A <= 8 and self.P <= 64 and \
-            (step_layout == "rows" or self.E >= 10240)
+            (step_layout == "rows" or self.E >= 7168)
         self.cfg = cfg
         flat = np.ascontiguousarray(np.concatenate([g.reshape(-1) for g in self.grids]).astype(np.uint8))
         hw = np.array([[g.shape[0], g.shape[1]] for g in self.grids], np.int32).reshape(-1)

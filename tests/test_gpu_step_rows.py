@@ -6,7 +6,7 @@ modes, both action formats, A < 5 / A = 5 / A = 8 (numpy's 8-partial sum), P fro
 wave's rows empty, and mixed maps.
 The oracle and golden-fixture tests run this kernel too (test_gpu_parity.py: test_vs_oracle_rows_layout,
 the "rows" cases of test_vs_oracle_map1 and test_mappo_rollout_golden); the default layout ("auto")
-picks it for full-batch steps of >= 10,240 envs (test_rows_auto_threshold)."""
+picks it for full-batch steps of >= 7,168 envs (test_rows_auto_threshold)."""
 import numpy as np
 import pytest
 
@@ -119,17 +119,17 @@ def test_rows_layout_refused_where_it_does_not_apply():
 
 
 def test_rows_auto_threshold():
-    """auto: one wave per env below 10,240 envs, four per wave from there on; same results."""
+    """auto: one wave per env below 7,168 envs, four per wave from there on; same results."""
     mg = _mg()
-    small = mg.BatchedEnv(grid("map1.txt"), 10239, 5, 50, 30, seed=1)
-    big = mg.BatchedEnv(grid("map1.txt"), 10240, 5, 50, 30, seed=1)
+    small = mg.BatchedEnv(grid("map1.txt"), 7167, 5, 50, 30, seed=1)
+    big = mg.BatchedEnv(grid("map1.txt"), 7168, 5, 50, 30, seed=1)
     assert not small.step_rows and big.step_rows
-    ref = mg.BatchedEnv(grid("map1.txt"), 10240, 5, 50, 30, seed=1, step_layout="wave")
+    ref = mg.BatchedEnv(grid("map1.txt"), 7168, 5, 50, 30, seed=1, step_layout="wave")
     for e in (big, ref):
         e.reset()
     gen = torch.Generator(device="cuda").manual_seed(12)
     for k in range(40):
-        acts = torch.randint(0, 15, (10240, 5), dtype=torch.uint8, device="cuda", generator=gen)
+        acts = torch.randint(0, 15, (7168, 5), dtype=torch.uint8, device="cuda", generator=gen)
         r1, s1, d1 = big.step(acts)
         r2, s2, d2 = ref.step(acts)
         assert torch.equal(r1, r2) and torch.equal(s1.view(torch.int32), s2.view(torch.int32)) and torch.equal(d1, d2)

@@ -459,15 +459,34 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
         td[c] = 0;
         tq[c] = 0;
         dirty[c] = false;
-        if (j < P) {
-            pk[c] = pkge[(uint32_t)j];
-            ps[c] = pste[(uint32_t)j];
-            if (STALE) td[c] = trke[(uint32_t)j];
+        if constexpr (NCH == 1) {
+            if (j < P) {
+                pk[c] = pkge[(uint32_t)j];
+                ps[c] = pste[(uint32_t)j];
+                if (STALE) td[c] = trke[(uint32_t)j];
+            }
+        } else {
+            // Several chunks: every lane loads (slot 0 where j >= P, discarded below).  As one
+            // exec-masked block per chunk, the copies out of each block waited for its loads, so
+            // each chunk's loads issued only after the previous chunk's had returned.
+            const uint32_t o = j < P ? (uint32_t)j : 0u;
+            pk[c] = pkge[o];
+            ps[c] = pste[o];
+            if (STALE) td[c] = trke[o];
         }
-        ps_in[c] = ps[c];
     }
     const u32x4 esv = esp[e];
     __builtin_amdgcn_sched_barrier(0);  // every load above is issued before any use
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        if constexpr (NCH > 1) {
+            const bool jv = c * WAVE + lane < P;
+            pk[c] = jv ? pk[c] : 0ull;
+            ps[c] = jv ? ps[c] : 0u;
+            td[c] = jv ? td[c] : 0ull;
+        }
+        ps_in[c] = ps[c];
+    }
     // The other kernel arguments, fetched now in one scalar batch while the state
     // loads are in flight, and pinned by ONE asm statement (one wait; separate pins let
     // the compiler wait after the first few and issue the rest behind that wait).  The

@@ -567,6 +567,24 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
             }
         }
 
+        // The shaped reward's candidates (tracker_prev's waiting entries, MAPPO/helper.py:257-369):
+        // pre-step state only, so computed here, where they can fill the movement's dependent
+        // readlane chain instead of waiting behind it.
+        bool wv[NCH];
+        int stc[NCH];
+        uint32_t klo[NCH];  // low key bits: order key << 10 | slot, or ~0 for no candidate
+        uint64_t wvm[NCH], anyw = 0;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const uint32_t f = ps0[c];
+            const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
+            wv[c] = waiting && pk_st(td[c]) <= t0;
+            stc[c] = pk_start(td[c]);
+            klo[c] = wv[c] ? (tq[c] << 10) | (uint32_t)(c * WAVE + lane) : 0xffffffffu;
+            wvm[c] = ballot(wv[c]);
+            anyw |= wvm[c];
+        }
+
         STAMP(3);
         // ---- movement (env.py:188-257) ----
         // moved = least fixed point of
@@ -818,20 +836,6 @@ __device__ __forceinline__ void step_body(const uint32_t* __restrict__ rob_pre, 
             const bool need_near = (Mact & Mmov & (Mpc0 | ~Mpres)) != 0u;
             const bool need_idle = (Mact & ~Mmov & MS & Mpc0) != 0u;
             const bool need_can = (Mact & Mop1 & Mpc0 & Mc0) != 0u;
-            bool wv[NCH];
-            int stc[NCH];
-            uint32_t klo[NCH];  // low key bits: order key << 10 | slot, or ~0 for no candidate
-            uint64_t wvm[NCH], anyw = 0;
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                const uint32_t f = ps0[c];
-                const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
-                wv[c] = waiting && pk_st(td[c]) <= t0;
-                stc[c] = pk_start(td[c]);
-                klo[c] = wv[c] ? (tq[c] << 10) | (uint32_t)(c * WAVE + lane) : 0xffffffffu;
-                wvm[c] = ballot(wv[c]);
-                anyw |= wvm[c];
-            }
             STAMP(7);
             // per-agent answers: bit masks in SGPRs, the nearest start cell written
             // into the agent's lane

@@ -100,6 +100,11 @@ def parse(argv=None):
                          "envs per wavefront where A <= 8 and P <= 64")
     ap.add_argument("--host-wait", default="auto", choices=("auto", "spin", "yield", "blocking"),
                     help="how the host waits for the GPU in synchronize (hipSetDeviceFlags schedule mode)")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="N > 1, config 2: skip the second timed region of 4,096 envs in total split over the ranks")
+    ap.add_argument("--gather", action="store_true",
+                    help="N > 1: after the timed regions, all-gather one step of critic vectors (the optional "
+                         "rollout collation, marl_gpu.dist.gather_rollout) and report its rate")
     ap.add_argument("--graph-only", action="store_true",
                     help="skip the eager, isolated-launch and floor legs (rocprof kernel-trace pass: the trace then "
                          "holds only the warmup and the timed graph replay, so its average is the timed region's)")
@@ -224,6 +229,18 @@ def cpu_baseline(args, grid, seeds0, budget_s, n_threads, E, map_name, host, wit
     return rec
 
 
+# The reference's own CPU figures (MAPPO/env_vectorized.py VectorizedEnv, env.step only, 4096 map1
+# envs), measured in the build container because the reference never travels to the GPU box
+# (BASELINE.md §2): static numbers, labelled as measured elsewhere -- not this host.
+REFERENCE_CPU = {
+    "what": "reference MAPPO/env_vectorized.py VectorizedEnv(Environment, 4096) map1 A=5 P=50 T=500, env.step only, "
+            "uniform random trainer-int actions, auto-reset",
+    "serial_1core": 195453.0, "processes_8": 1650597.0, "unit": "agent-steps/s",
+    "host": "build container: Intel Xeon, 8 cores, 1 thread/core, Python 3.10.12, NumPy 2.2.6",
+    "source": "BASELINE.md section 2 (measured in the build container, NOT on this GPU host: the reference does not "
+              "travel; cpu_baseline is the same workload through the C restatement timed on this host)",
+}
+
 HIP_SCHEDULE = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}   # hipDeviceSchedule* flags
 
 
@@ -244,6 +261,63 @@ def device_record(rank, local, dev_index):
                               getattr(pr, "pci_device_id", 0))
     return {"rank": rank, "local_rank": local, "device": dev_index, "pci": bus, "name": pr.name,
             "arch": getattr(pr, "gcnArchName", "")}
+
+
+def strong_region(args, D, marl_gpu, grid, rank, world, dev, graph_region, obs_dims, G, K, dist):
+    """4,096 envs in total over the ranks (the metric's workload at N GPUs, strong scaling): each
+    rank steps its shard_strong share (global ids and seeds as one process would give them), timed
+    like the headline region; the MAX over ranks of the wall time sets the rate."""
+    A, P = args.agents, args.packages
+    total = 4096
+    ids, seeds = D.shard_strong(total, rank, world, args.seed)
+    E = len(ids)
+    env = marl_gpu.BatchedEnv(grid, E, A, P, args.T, seeds=seeds, tracker="mappo", shaping="mappo", device=dev,
+                              step_layout=args.step_layout, **obs_dims)
+    env.reset()
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    acts = torch.randint(0, 15, (G, E, A), generator=gen, device=dev, dtype=torch.int32).to(torch.uint8)
+    out = (torch.zeros(E, dtype=torch.float64, device=dev), torch.zeros(E, dtype=torch.float32, device=dev),
+           torch.zeros(E, dtype=torch.uint8, device=dev))
+    wall, gpu_ms = graph_region(lambda k: env.step(acts[k % G], auto_reset=True, out=out))
+    layout = env.last_step_layout()
+    wall_f = 0.0
+    if not args.no_floor and not args.graph_only:
+        wall_f, _ = graph_region(lambda k: env.step_floor())
+    mx = D.max_over_ranks([wall, wall_f], device=dev if args.backend == "nccl" else None)
+    env.close()
+    sizes = [len(D.shard_strong(total, r, world, 0)[0]) for r in range(world)]
+    return {"total_envs": total, "envs_per_rank": sizes, "value": total * A * K / mx[0], "unit": "agent-steps/s",
+            "ms_per_step": mx[0] / K * 1e3, "gpu_event_ms_per_step_rank0": gpu_ms / K,
+            "launch_floor_ms_per_step": (mx[1] / K * 1e3) if wall_f else None,
+            "step_layout": layout, "steps": K, "scaling": "strong",
+            "note": "second timed region after the weak one: BASELINE.json's metric workload (4096 map1 envs) split "
+                    "over the ranks, replayed and timed like the headline (graphs, warmup, barrier, MAX over ranks)"}
+
+
+def gather_leg(args, D, env, run0, dev, dist, world, reps=20):
+    """The optional RCCL rollout collation, off the timed step region: the critic
+    vectors of this rank's envs for one step (convert_global_state's vector, 1301 floats per env at
+    the MAPPO dims) all-gathered to every rank with marl_gpu.dist.gather_rollout."""
+    _, b0, n0 = run0
+    cv = env.build_obs(b0, n0, which=("critic_vec",))["critic_vec"]
+    torch.cuda.synchronize()
+    full = D.gather_rollout(cv)   # warm (communicator set-up)
+    full = D.gather_rollout(cv)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        full = D.gather_rollout(cv)
+    torch.cuda.synchronize()
+    dt = D.max_over_ranks([time.perf_counter() - t0], device=dev if args.backend == "nccl" else None)[0]
+    per = dt / reps
+    nbytes = full.numel() * full.element_size()
+    return {"tensor": f"critic_vec [{n0}, {cv.shape[1]}] float32 per rank", "bytes_per_rank": cv.numel() * 4,
+            "gathered_bytes": nbytes, "ms_per_gather": per * 1e3, "gathered_GBps": nbytes / per / 1e9,
+            "received_GBps_per_rank": nbytes * (world - 1) / world / per / 1e9, "reps": reps,
+            "backend": dist.get_backend(),
+            "note": ("RCCL all_gather_into_tensor on device tensors (xGMI)" if dist.get_backend() == "nccl" else
+                     "gloo: through host memory -- rehearsal of the code path only, not an xGMI figure")}
 
 
 def main(argv=None):
@@ -390,6 +464,9 @@ def main(argv=None):
         wall = stop_clock(t0)
         gpu_ms = ev0.elapsed_time(ev1)
 
+    # the layout of the launches just timed, as the engine recorded it (step_obs: its fused wave kernel)
+    layout = "wave" if obs_cfg else env.last_step_layout()
+
     # ---- eager throughput (same kernels, one ctypes launch per step) ----
     wall_eager = None
     if not args.graph_only:
@@ -447,6 +524,17 @@ def main(argv=None):
         wall_f = float(t[2]) if wall_f is not None else None
         wall_floor = float(t[3]) if wall_floor is not None else None
 
+    # ---- N > 1, config 2: a second timed region on the metric's own workload -- 4,096 envs in
+    # TOTAL split over the ranks (strong scaling; shard_strong, seeds 42 + global id)
+    strong = None
+    if dist is not None and world > 1 and args.config == "2" and args.total_envs == 0 and not args.no_strong:
+        strong = strong_region(args, D, marl_gpu, grids[0], rank, world, dev, graph_region, obs_dims, G, K, dist)
+
+    # ---- optional rollout collation (N > 1): one step of critic vectors all-gathered over the ranks
+    gather = None
+    if args.gather and dist is not None and world > 1:
+        gather = gather_leg(args, D, env, runs[0], dev, dist, world)
+
     total_agent_steps = E_all * A * K
     value = total_agent_steps / wall
     if rank == 0:
@@ -467,7 +555,7 @@ def main(argv=None):
                 for rec in tj.get("records", []):
                     rows_rec = "k_step_rows" in rec.get("kernel", "")
                     if rec.get("config") == want and bool(rec.get("obs")) == obs_cfg and \
-                            (obs_cfg or rows_rec == env.step_rows):   # the PMC pass of the kernel timed here
+                            (obs_cfg or rows_rec == (layout == "rows")):   # the PMC pass of the kernel timed here
                         traffic, traffic_rec = rec.get("hbm_bytes_per_launch"), rec
             except (OSError, ValueError):
                 traffic = None
@@ -480,13 +568,8 @@ def main(argv=None):
             cpu = cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, nt, Ec, args.maps[m0], host, obs_cfg)
             cpu1 = cpu if nt == 1 else cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, 1, Ec,
                                                      args.maps[m0], host, obs_cfg)
-        std = (A, P) == (CONFIGS[args.config]["agents"], CONFIGS[args.config]["packages"])
-        kname = {"2": "mdl::k_step<true, 1, false, 5>", "3": "mdl::k_step_obs<true, 5>",
-                 "4": "mdl::k_step<true, 1, false, 5> (mixed maps)",
-                 "5": "mdl::k_step<true, 2, false, 16>"}[args.config] if std else "mdl::k_step"
-        if env.step_rows and args.config != "3":
-            kname = "mdl::k_step_rows<true, 5>" if A == 5 else "mdl::k_step_rows<true, 8>"
-            kname += " (mixed maps)" if args.config == "4" else ""
+        # the kernel the engine launched (its own record and symbol: no Python mirror of its rules)
+        kname = env.step_kernel_name(layout, with_obs=obs_cfg) + (" (mixed maps)" if len(grids) > 1 else "")
         ms_step = wall / K * 1e3
         floor = None
         if wall_floor is not None:
@@ -530,8 +613,9 @@ def main(argv=None):
                        "obs_dims": ({"actor_vec": env.actor_vec_dim, "critic_vec": env.critic_vec_dim,
                                      "obs_bytes_per_env_step": obs_bytes_env} if obs_cfg else None),
                        "parallelism": f"env-shard x{world}",
-                       "step_layout": ("rows (4 envs per wavefront)" if env.step_rows and not obs_cfg
-                                       else "wave (1 env per wavefront)")},
+                       "step_layout": ("rows (4 envs per wavefront)" if layout == "rows"
+                                       else "wave (1 env per wavefront)"),
+                       "step_layout_source": "engine (mdl_last_step_layout of the timed launches)"},
             "gpu_event_ms_per_step": gpu_ms / K,
             "eager": None if wall_eager is None else {"value": total_agent_steps / wall_eager,
                                                        "ms_per_step": wall_eager / K * 1e3},
@@ -551,6 +635,9 @@ def main(argv=None):
                         "actions (bit-exact with K mdl_step calls); not the API path, not the headline value"},
             "cpu_baseline": cpu,
             "cpu_baseline_1thread": cpu1,
+            "reference_cpu": REFERENCE_CPU,
+            "strong_4096": strong,
+            "rollout_gather": gather,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -337,6 +337,16 @@ int mdl_rank_table(int32_t H, int32_t W, uint16_t* out);
 
 /* Introspection */
 int mdl_get_config(const MdlEngine* eng, MdlConfig* out);
+/* The step layout (MDL_STEP_LAYOUT_WAVE or _ROWS) mdl_step launches for a call over n envs
+ * (use_ids = 0: the full batch, n ignored as in mdl_step; use_ids = 1: an env_ids subset of n,
+ * always WAVE) -- the engine's own decision, the one mdl_step takes. */
+int mdl_step_layout(const MdlEngine* eng, int32_t n, int32_t use_ids, int32_t* layout);
+/* The layout of the last mdl_step launch on this engine (0 before the first one). */
+int mdl_last_step_layout(const MdlEngine* eng, int32_t* layout);
+/* The symbol (as rocprof reports it, e.g. "mdl::k_step<true, 1, false, 5>") of the kernel mdl_step
+ * launches in `layout` (WAVE / ROWS), or, with with_obs, of mdl_step_obs's step launch (its fused
+ * step + observation kernel where it applies).  NUL-terminated into out[cap]. */
+int mdl_step_kernel_name(const MdlEngine* eng, int32_t layout, int32_t with_obs, char* out, int32_t cap);
 int mdl_obs_dims(const MdlEngine* eng, int32_t* actor_vec_dim, int32_t* critic_vec_dim);
 const char* mdl_last_error(void);
 const char* mdl_version(void);

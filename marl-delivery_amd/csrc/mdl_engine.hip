@@ -129,6 +129,13 @@ struct MdlEngine {
     // config 4's 65,536 28.7 vs 21.1; profiles/r05/rows_ab.txt).
     static constexpr int ROWS_MIN_ENVS = 7168;
     bool rows_for(int n) const { return step_rows && (rows_forced || n >= ROWS_MIN_ENVS); }
+    // the layout mdl_step launches for a call over n envs (with an id list: always one wave per env)
+    int32_t layout_for(int n, bool ids) const { return (!ids && rows_for(n)) ? MDL_STEP_LAYOUT_ROWS : MDL_STEP_LAYOUT_WAVE; }
+    int32_t last_step_layout = 0;   // MDL_STEP_LAYOUT_* of the last mdl_step launch (0: none yet)
+    // A synchronous host-mapped call whose wait timed out leaves its launch queued on `hung`: until that
+    // stream has drained, no call may rewrite the mailbox / arena inputs that launch still reads.
+    bool poisoned = false;
+    hipStream_t hung = nullptr;
     int wpb_step = 1, wpb_obs = 1;
     int obs_rank_lds = 0;   // small builder: LDS bytes of the largest map's rank table (0: ranks read from L2)
     int n_cu = 0;   // compute units of the device (step_wpb)
@@ -539,7 +546,9 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
     if (n < 0 || n > eng->p.E) return fail("mdl_step: n=%d out of range", n);
     if (n == 0) return 0;
     DeviceGuard dg(eng->device);
-    if (!env_ids && eng->rows_for(n)) {
+    const int32_t layout = eng->layout_for(n, env_ids != nullptr);
+    eng->last_step_layout = layout;
+    if (layout == MDL_STEP_LAYOUT_ROWS) {
         HIPCHK(mdl::launch_step_rows(eng->p, actions, action_format, n, auto_reset, r_env, r_shaped, done,
                                      step_wpb(n, eng->n_cu, eng->lds_rows, eng->p.P), eng->lds_rows,
                                      (hipStream_t)stream));
@@ -673,7 +682,20 @@ int mail_check_ids(MdlEngine* eng, int32_t n, int32_t use_ids, const char* who) 
 // few milliseconds), so a GPU that never publishes must not hang the process: past
 // SPIN_LIMIT_S seconds with the stream still busy the call fails instead of spinning on.
 constexpr double SPIN_LIMIT_S = 60.0;
-int spin_wait(volatile const int32_t* seq, int32_t want, hipStream_t s, const char* who) {
+// Refuses host-mapped I/O while a timed-out call's launch may still be queued (spin_wait): that
+// launch reads the mailbox / arena inputs and publishes a sequence value, so a new call could hand
+// it new inputs or misread its completion.  Cleared once the stream it was queued on has drained.
+int host_io_ok(MdlEngine* eng, const char* who) {
+    if (!eng->poisoned) return 0;
+    const hipError_t q = hipStreamQuery(eng->hung);
+    if (q == hipSuccess) {
+        eng->poisoned = false;
+        return 0;
+    }
+    return fail("%s: an earlier synchronous call on this engine timed out with its launch still queued (%s); "
+                "refused until that stream has drained", who, q == hipErrorNotReady ? "still running" : hipGetErrorString(q));
+}
+int spin_wait(MdlEngine* eng, volatile const int32_t* seq, int32_t want, hipStream_t s, const char* who) {
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned long spins = 1;; spins++) {
         if (*seq == want) return 0;
@@ -683,8 +705,12 @@ int spin_wait(volatile const int32_t* seq, int32_t want, hipStream_t s, const ch
             if (q != hipSuccess && q != hipErrorNotReady) return fail("%s: %s", who, hipGetErrorString(q));
             if (q == hipSuccess && *seq != want) return fail("%s: the call finished without publishing", who);
             const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            if (el > SPIN_LIMIT_S)
-                return fail("%s: no completion after %.0f s (stream still busy): giving up the wait", who, el);
+            if (el > SPIN_LIMIT_S) {
+                eng->poisoned = true;   // the launch may still read the host-mapped inputs: see host_io_ok
+                eng->hung = s;
+                return fail("%s: no completion after %.0f s (stream still busy): giving up the wait; host-mapped "
+                            "calls on this engine are refused until that stream has drained", who, el);
+            }
         }
     }
 }
@@ -697,7 +723,7 @@ int mail_finish(MdlEngine* eng, int32_t n, int32_t use_ids, hipStream_t s, const
     const unsigned base = eng->mail_waves;
     HIPCHK(mdl::launch_mail_export(eng->p, use_ids ? m.ids : nullptr, n, rows, eng->mail_ctr, base, want, s));
     eng->mail_waves += mdl::mail_export_waves(n);   // the device counter's value after this launch
-    return spin_wait(m.seq, want, s, who);
+    return spin_wait(eng, m.seq, want, s, who);
 }
 }  // namespace
 
@@ -705,6 +731,7 @@ int mdl_mail_step(MdlEngine* eng, int32_t n, int32_t use_ids, int32_t auto_reset
     if (!eng) return fail("mdl_mail_step: null engine");
     if (!eng->seeded) return fail("mdl_mail_step: engine not seeded (call mdl_seed first)");
     if (mail_check_ids(eng, n, use_ids, "mdl_mail_step")) return -1;
+    if (host_io_ok(eng, "mdl_mail_step")) return -1;
     if (n == 0) return 0;
     DeviceGuard dg(eng->device);
     hipStream_t s = (hipStream_t)stream;
@@ -716,13 +743,14 @@ int mdl_mail_step(MdlEngine* eng, int32_t n, int32_t use_ids, int32_t auto_reset
                                  m.done, step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, rows,
                                  eng->mail_ctr, eng->mail_waves, want, s));
     eng->mail_waves += (unsigned)n;   // the n waves of rows [0, n) counted themselves
-    return spin_wait(m.seq, want, s, "mdl_mail_step");
+    return spin_wait(eng, m.seq, want, s, "mdl_mail_step");
 }
 
 int mdl_mail_reset(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream) {
     if (!eng) return fail("mdl_mail_reset: null engine");
     if (!eng->seeded) return fail("mdl_mail_reset: engine not seeded (call mdl_seed first)");
     if (mail_check_ids(eng, n, use_ids, "mdl_mail_reset")) return -1;
+    if (host_io_ok(eng, "mdl_mail_reset")) return -1;
     if (n == 0) return 0;
     DeviceGuard dg(eng->device);
     hipStream_t s = (hipStream_t)stream;
@@ -732,6 +760,7 @@ int mdl_mail_reset(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream) {
 
 int mdl_host_arena(MdlEngine* eng, int64_t bytes, void** out) {
     if (!eng || !out || bytes < 0) return fail("mdl_host_arena: bad argument");
+    if (host_io_ok(eng, "mdl_host_arena")) return -1;   // a queued launch may still use the arena
     if (!eng->arena || (size_t)bytes > eng->arena_bytes) {
         size_t cap = 64 * 1024;
         while (cap < (size_t)bytes) cap *= 2;
@@ -755,17 +784,19 @@ int mdl_host_arena(MdlEngine* eng, int64_t bytes, void** out) {
 int mdl_host_wait(MdlEngine* eng, void* stream) {
     if (!eng) return fail("mdl_host_wait: null engine");
     if (!eng->arena) return fail("mdl_host_wait: call mdl_host_arena first");
+    if (host_io_ok(eng, "mdl_host_wait")) return -1;
     DeviceGuard dg(eng->device);
     hipStream_t s = (hipStream_t)stream;
     int32_t* seq = (int32_t*)eng->arena;
     const int32_t want = eng->arena_seq = (eng->arena_seq % 0x7ffffff0) + 1;
     HIPCHK(mdl::launch_publish(seq, want, s));
-    return spin_wait(seq, want, s, "mdl_host_wait");
+    return spin_wait(eng, seq, want, s, "mdl_host_wait");
 }
 
 int mdl_mail_export(MdlEngine* eng, int32_t n, int32_t use_ids, void* stream) {
     if (!eng) return fail("mdl_mail_export: null engine");
     if (mail_check_ids(eng, n, use_ids, "mdl_mail_export")) return -1;
+    if (host_io_ok(eng, "mdl_mail_export")) return -1;
     if (n == 0) return 0;
     DeviceGuard dg(eng->device);
     return mail_finish(eng, n, use_ids, (hipStream_t)stream, "mdl_mail_export");
@@ -968,7 +999,7 @@ struct HostCall {
         if (!on) return 0;
         eng->arena_seq = pb.value;
         eng->arena_waves += waves;
-        return spin_wait(pb.seq, pb.value, s, who);
+        return spin_wait(eng, pb.seq, pb.value, s, who);
     }
 };
 
@@ -977,6 +1008,7 @@ int views_features(MdlEngine* eng, const int32_t* views, const int64_t* offsets,
                    float* vec, float* gmap, float* gvec, void* stream, bool host, const char* who) {
     if (!eng || !views || !offsets) return fail("%s: null argument", who);
     if (host && !eng->arena) return fail("%s: call mdl_host_arena first", who);
+    if (host && host_io_ok(eng, who)) return -1;
     if (n_views < 0 || max_slots < 0 || max_slots > 4096) return fail("%s: bad sizes", who);
     if (MO < 0 || MP < 0 || MR < 0 || MPs < 0) return fail("%s: negative slot count", who);
     if (n_views == 0) return 0;
@@ -999,6 +1031,7 @@ int views_shaped(MdlEngine* eng, const int32_t* prev_views, const int64_t* prev_
     if (!eng || !prev_views || !prev_offsets || !cur || !cur_offsets || !actions || !act_offsets || !g || !out)
         return fail("%s: null argument", who);
     if (host && !eng->arena) return fail("%s: call mdl_host_arena first", who);
+    if (host && host_io_ok(eng, who)) return -1;
     if (n < 0 || max_slots < 0 || max_slots > 4096) return fail("%s: bad sizes", who);
     if (n == 0) return 0;
     mdl::ShapingConsts C;
@@ -1022,6 +1055,7 @@ int mdl_host_view_features(MdlEngine* eng, const int32_t* rec, int32_t words, in
     const char* who = "mdl_host_view_features";
     if (!eng || !rec) return fail("%s: null argument", who);
     if (!eng->arena) return fail("%s: call mdl_host_arena first", who);
+    if (host_io_ok(eng, who)) return -1;
     if (words < 4 || words > MDL_VIEW_INLINE_WORDS)
         return fail("%s: a record of %d words (inline records hold 4..%d)", who, words, MDL_VIEW_INLINE_WORDS);
     const int A = rec[1], ns = rec[2], map = rec[3];
@@ -1046,6 +1080,7 @@ int mdl_host_view_shaped_reward(MdlEngine* eng, const int32_t* prev_view, int32_
     const char* who = "mdl_host_view_shaped_reward";
     if (!eng || !prev_view || !cur || (!actions && n_actions > 0) || !out) return fail("%s: null argument", who);
     if (!eng->arena) return fail("%s: call mdl_host_arena first", who);
+    if (host_io_ok(eng, who)) return -1;
     if (prev_words < 4 || cur_words < 2 || n_actions < 0) return fail("%s: bad sizes", who);
     const int A = prev_view[1], ns = prev_view[2];
     if (A < 0 || A > MDL_MAX_ROBOTS || ns < 0 || 4 + 3 * A + 8 * ns > prev_words)
@@ -1165,6 +1200,33 @@ int mdl_rank_table(int32_t H, int32_t W, uint16_t* out) {
 int mdl_get_config(const MdlEngine* eng, MdlConfig* out) {
     if (!eng || !out) return fail("mdl_get_config: null argument");
     *out = eng->cfg;
+    return 0;
+}
+
+int mdl_step_layout(const MdlEngine* eng, int32_t n, int32_t use_ids, int32_t* layout) {
+    if (!eng || !layout) return fail("mdl_step_layout: null argument");
+    if (n < 0 || n > eng->p.E) return fail("mdl_step_layout: n=%d out of range", n);
+    *layout = eng->layout_for(use_ids ? n : eng->p.E, use_ids != 0);
+    return 0;
+}
+
+int mdl_step_kernel_name(const MdlEngine* eng, int32_t layout, int32_t with_obs, char* out, int32_t cap) {
+    if (!eng || !out || cap < 1) return fail("mdl_step_kernel_name: bad argument");
+    if (layout != MDL_STEP_LAYOUT_WAVE && layout != MDL_STEP_LAYOUT_ROWS)
+        return fail("mdl_step_kernel_name: layout %d is not WAVE or ROWS", layout);
+    if (layout == MDL_STEP_LAYOUT_ROWS && (with_obs || !eng->step_rows))
+        return fail("mdl_step_kernel_name: no rows-layout launch in this configuration");
+    // mdl_step_obs's one-launch form (else it is mdl_step's wave kernel + the builder)
+    const bool obs = with_obs && eng->p.obs_small && eng->p.A <= 8 && eng->p.P <= 64 &&
+                     std::max(eng->lds_step, eng->lds_obs) <= LDS_BUDGET;
+    const int k = mdl::step_kernel_name(eng->p, layout == MDL_STEP_LAYOUT_ROWS, obs, out, cap);
+    if (k < 0 || k >= cap) return fail("mdl_step_kernel_name: buffer of %d bytes too small", cap);
+    return 0;
+}
+
+int mdl_last_step_layout(const MdlEngine* eng, int32_t* layout) {
+    if (!eng || !layout) return fail("mdl_last_step_layout: null argument");
+    *layout = eng->last_step_layout;
     return 0;
 }
 

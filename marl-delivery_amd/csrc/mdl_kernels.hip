@@ -1838,6 +1838,16 @@ hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt,
     return hipGetLastError();
 }
 
+// (the dispatch of launch_step_rows above, launch_step_obs and launch_step_t below)
+int step_kernel_name(const DevParams& p, bool rows, bool obs, char* out, int cap) {
+    const char* st = p.stale ? "true" : "false";
+    if (rows) return snprintf(out, (size_t)cap, "mdl::k_step_rows<%s, %d, 4>", st, p.A == 5 ? 5 : 8);
+    if (obs) return snprintf(out, (size_t)cap, "mdl::k_step_obs<%s, %d>", st, p.A == 5 ? 5 : 8);
+    const int nch = nch_for(p.P);
+    const int au = (nch <= 2 && p.A == 5) ? 5 : (nch <= 2 && p.A == 16) ? 16 : p.A <= 8 ? 8 : 0;
+    return snprintf(out, (size_t)cap, "mdl::k_step<%s, %d, false, %d>", st, nch, au);
+}
+
 hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s, bool rows) {
     StepArgs a{};
     a.p = p;

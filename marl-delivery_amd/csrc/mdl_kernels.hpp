@@ -19,6 +19,10 @@ hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, cons
 // k_step_rows (mdl_step_rows.hpp): a full-batch step with four envs per wavefront, one per 16-lane
 // row; A <= 8, P <= 64 (step_rows_ok).  lds: the per-wave slice (step_rows_lds).
 bool step_rows_ok(int A, int P);
+// The symbol (as rocprof names it) of the step kernel a launch takes: launch_step_rows (rows),
+// launch_step_obs (obs: the fused step + observation kernel) or launch_step.  Mirrors their
+// dispatch; bench.py labels its roofline record with it.  Returns snprintf's count.
+int step_kernel_name(const DevParams& p, bool rows, bool obs, char* out, int cap);
 size_t step_rows_lds(int P);
 hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
                             float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s);

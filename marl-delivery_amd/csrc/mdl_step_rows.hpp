@@ -7,8 +7,8 @@
 // exec-mask handling, readlane chains, loop control) once per env.  The step is issue bound at
 // every measured batch (profiles/r05: ~3 cycles per wave instruction per SIMD, 4096 to 131,072
 // envs).  Here env r of the wave lives on lanes 16r..16r+15: robot a on row lane a (A <= AU <= 8),
-// package j on row lane j & 15 of chunk j >> 4 (NC = 4 chunks, P <= 64; the code is written for
-// NC = 8 too, which measured slower than k_step at P = 100 and is not instantiated).  Everything an env does is
+// package j on row lane j & 15 of chunk j >> 4 (NC = 4 chunks, P <= 64; an eight-chunk form for
+// P <= 128 measured slower than k_step at P = 100 and was removed, profiles/r05/rows_ab.txt).  Everything an env does is
 // row-local: broadcasts are DPP row_newbcast (one VALU op, no SGPR), minima are four in-row DPP
 // stages, a ballot's row part is one 64-bit vector shift -- and each of those instructions serves
 // four envs.  The scalar instructions are shared by the four envs as well.
@@ -20,7 +20,7 @@
 #pragma once
 
 constexpr int ROW = 16;        // lanes per env
-// package chunks per lane: NC = 4 (P <= 64) or 8 (P <= 128), a template parameter of the kernel
+// package chunks per lane: NC = 4 (P <= 64), the only form built (a template parameter of the kernel)
 
 // lane J of this lane's row, on every lane of the row (DPP row_newbcast, gfx90a+)
 template <int J>
@@ -85,7 +85,6 @@ __host__ __device__ constexpr size_t rows_scratch_bytes(int NC) { return (size_t
 // one flag byte per package slot, a lane's NC slots in one load
 template <int NC> struct FlagWord;
 template <> struct FlagWord<4> { typedef uint32_t T; };
-template <> struct FlagWord<8> { typedef uint64_t T; };
 
 // (93 VGPRs, 5 waves per SIMD.  Capping it at 6 waves (79 VGPRs) was 1 % faster on config 4 and 3-6 %
 // slower at 4,096-16,384 envs, at 7 waves 20 % slower: profiles/r05/rows_ab.txt.)
@@ -98,7 +97,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
                                                    const uint8_t* __restrict__ act_pre, uint32_t ap, uint32_t nw,
                                                    StepArgs args) {
     static_assert(AU >= 1 && AU <= 8, "k_step_rows: A <= 8");
-    static_assert(NC == 4 || NC == 8, "k_step_rows: P <= 64 or P <= 128");
+    static_assert(NC == 4, "k_step_rows: P <= 64 (the only form built and tested)");
     constexpr uint32_t NONE = 255u;   // no package slot (slots < 16 * NC <= 128)
     extern __shared__ __align__(16) unsigned char smem[];
     const DevParams& p = args.p;
@@ -164,8 +163,9 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     const uint64_t tot_rec = live ? tot_ld : 0ull;
     // Slots without a package (j >= P, or a row past n) hold sentinels that fail every test by
     // themselves, so only the loads and the stores test the slot's existence: status delivered (the
-    // all-delivered test passes over them; not waiting, not present), start time 0xffff (never
-    // spawned or inserted: t < 0xffff), start cell 0xffff (no cell of a map of at most 255 rows).
+    // all-delivered test passes over them; not waiting, not present), start time 0xffff (no spawn
+    // or insert while t1 < 0xffff; past that only the stores' existence test keeps them out of
+    // memory), start cell 0xffff (no cell of a map of at most 255 rows).
 #pragma unroll
     for (int c = 0; c < NC; c++) {
         pk[c] = pv[c] ? pk[c] : ~0ull;
@@ -576,10 +576,12 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     for (int c = 0; c < NC; c++) {
         const int j = c * ROW + rl;
         const uint32_t o = (uint32_t)(r * P + j) & 0x1ffu;
-        // a sentinel slot's state word never changes and it is never inserted, so only the reset
-        // row's table store tests the slot's existence
-        if (ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
+        // Every store tests the slot's existence (pv: j < P in a live row).  A sentinel slot's start
+        // time 0xffff equals t1 once a done env steps on without reset to t = 65535, which "spawns"
+        // it (and inserts it into the stale tracker); its masked offset then names the next env's
+        // slot, or lies past the allocation for the last env.  (k_step guards its stores with j < P.)
+        if (pv[c] && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
         if (rrow && j < P) (pkgw + eb)[o] = pk[c];
-        if (STALE && dirty[c]) (trkw + eb)[o] = td[c];
+        if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
     }
 }

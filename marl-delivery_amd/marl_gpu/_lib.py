@@ -111,6 +111,9 @@ SIGNATURES = {
     "mdl_rank_table": (C.c_int, [_i32, _i32, _vp]),
     "mdl_get_config": (C.c_int, [_vp, C.POINTER(MdlConfig)]),
     "mdl_obs_dims": (C.c_int, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "mdl_step_layout": (C.c_int, [_vp, _i32, _i32, C.POINTER(C.c_int32)]),
+    "mdl_last_step_layout": (C.c_int, [_vp, C.POINTER(C.c_int32)]),
+    "mdl_step_kernel_name": (C.c_int, [_vp, _i32, _i32, C.c_char_p, _i32]),
     "mdl_last_error": (C.c_char_p, []),
     "mdl_version": (C.c_char_p, []),
 }

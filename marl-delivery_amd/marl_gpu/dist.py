@@ -90,10 +90,39 @@ def sum_over_ranks(values, device=None):
     return [float(x) for x in t.tolist()]
 
 
-def gather_rollout(t: torch.Tensor):
-    """All-gather a per-rank rollout tensor along dim 0 (collation for one learner)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+def gather_rollout(t: torch.Tensor, group=None):
+    """All-gather a per-rank rollout tensor along dim 0, in rank order: the collation of every
+    env's buffers for one learner (the reference's trainer stacks its per-env buffers on one host,
+    MAPPO/trainer.py:172-286).  Shards may differ in their leading size (``shard_strong`` gives the
+    lower ranks the remainder): the sizes are all-gathered first, every rank's part is padded to
+    the largest, and the padding is dropped from the result.  The trailing dims must agree.  On
+    RCCL the collective runs on the device tensors (one all_gather_into_tensor over xGMI); gloo
+    has no device all-gather, so a CUDA tensor goes through host memory there (rehearsal only).
+    Off the step path: one call per rollout, not per step."""
+    if not (dist.is_available() and dist.is_initialized()):
         return t
-    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
-    dist.all_gather(parts, t.contiguous())
-    return torch.cat(parts, 0)
+    ws = dist.get_world_size(group)
+    if ws == 1:
+        return t
+    t = t.contiguous()
+    host = dist.get_backend(group) == "gloo" and t.is_cuda
+    dev = torch.device("cpu") if host else t.device
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(ws)]
+    dist.all_gather(ns, n, group=group)
+    sizes = [int(x.item()) for x in ns]
+    mx = max(sizes)
+    src = t.to(dev) if host else t
+    if t.shape[0] < mx:   # pad this rank's part to the common size
+        pad = torch.zeros((mx - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        src = torch.cat([src, pad], 0)
+    if host:
+        parts = [torch.empty_like(src) for _ in range(ws)]
+        dist.all_gather(parts, src, group=group)
+        flat = torch.cat(parts, 0)
+    else:
+        flat = torch.empty((ws * mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        dist.all_gather_into_tensor(flat, src, group=group)
+    if min(sizes) < mx:
+        flat = torch.cat([flat[r * mx:r * mx + sizes[r]] for r in range(ws)], 0)
+    return flat.to(t.device) if host else flat

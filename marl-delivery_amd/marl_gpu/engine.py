@@ -104,9 +104,6 @@ class BatchedEnv:
         cfg.max_robots_state, cfg.max_packages_state = self.MR, self.MPs
         cfg.obs_builder = OBS_BUILDERS[obs_builder]
         cfg.step_layout = STEP_LAYOUTS[step_layout]
-        # whether a full-batch step runs four envs per wavefront (the engine's rule: MdlEngine::rows_for)
-        self.step_rows = step_layout != "wave" and self.A <= 8 and self.P <= 64 and \
-            (step_layout == "rows" or self.E >= 7168)
         self.cfg = cfg
         flat = np.ascontiguousarray(np.concatenate([g.reshape(-1) for g in self.grids]).astype(np.uint8))
         hw = np.array([[g.shape[0], g.shape[1]] for g in self.grids], np.int32).reshape(-1)
@@ -125,6 +122,8 @@ class BatchedEnv:
         av, cv = C.c_int32(), C.c_int32()
         check(lib().mdl_obs_dims(self._h, C.byref(av), C.byref(cv)))
         self.actor_vec_dim, self.critic_vec_dim = av.value, cv.value
+        # whether a full-batch step runs four envs per wavefront: the engine's own decision
+        self.step_rows = self.step_layout() == "rows"
         if seeds is None:
             seeds = [int(seed) + i for i in range(self.E)]
         self.seeds = np.ascontiguousarray(np.asarray(seeds, np.int64) & 0xFFFFFFFF).astype(np.uint32)
@@ -339,6 +338,30 @@ class BatchedEnv:
                                    int(bool(auto_reset)), ptr(r), ptr(sh), ptr(d), self._stream()), "mdl_step_fused")
         self._keep = (ids, actions)
         return r, sh, d
+
+    def step_layout(self, n: int | None = None) -> str:
+        """The layout ``step`` launches ("wave": one env per wavefront, "rows": four) for the full
+        batch (n None) or an ``env_ids`` subset of n envs -- asked of the engine (mdl_step_layout),
+        which takes the same decision inside mdl_step."""
+        lay = C.c_int32()
+        check(lib().mdl_step_layout(self._h, self.E if n is None else int(n), 0 if n is None else 1,
+                                    C.byref(lay)), "mdl_step_layout")
+        return {_lib.MDL_STEP_LAYOUT_WAVE: "wave", _lib.MDL_STEP_LAYOUT_ROWS: "rows"}[lay.value]
+
+    def step_kernel_name(self, layout: str | None = None, with_obs: bool = False) -> str:
+        """The kernel symbol (as rocprof names it) ``step`` launches in ``layout`` (default: the
+        full batch's), or ``step_obs``'s step launch with ``with_obs`` -- from the engine."""
+        lay = ("wave" if with_obs else self.step_layout()) if layout is None else layout
+        buf = C.create_string_buffer(128)
+        check(lib().mdl_step_kernel_name(self._h, STEP_LAYOUTS[lay], 1 if with_obs else 0, buf, 128),
+              "mdl_step_kernel_name")
+        return buf.value.decode()
+
+    def last_step_layout(self) -> str | None:
+        """The layout of the last ``step`` launch (None before the first), as the engine recorded it."""
+        lay = C.c_int32()
+        check(lib().mdl_last_step_layout(self._h, C.byref(lay)), "mdl_last_step_layout")
+        return {0: None, _lib.MDL_STEP_LAYOUT_WAVE: "wave", _lib.MDL_STEP_LAYOUT_ROWS: "rows"}[lay.value]
 
     def step_floor(self, n: int | None = None):
         """Measurement aid: one launch of an empty kernel in ``step``'s launch shape over n envs

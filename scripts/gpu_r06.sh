@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 5 GPU pass: the GPU suite (new tests first), smoke, the driver's default bench line,
+# Round 6 GPU pass: the GPU suite (new tests first), smoke, the driver's default bench line,
 # the plain multi-rank command, config 3's line.  Each GPU step has its own time limit; the
 # first failure ends the call.
 set -u
-O=gpurun_out/r05/${TAG:-pass}
+O=gpurun_out/r06/${TAG:-pass}
 mkdir -p $O
 run() {   # name seconds cmd...
   local n=$1 s=$2; shift 2

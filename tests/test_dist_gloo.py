@@ -141,3 +141,44 @@ def test_shard_partitions():
             all_maps += em
         assert all_ids == list(range(65536))
         assert all_maps == sum([[m] * n for m, n in enumerate(D.map_group_sizes(65536, 5))], [])
+
+
+def _gather_worker(rank, world, port, total, out_q):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "marl-delivery_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from marl_gpu import dist as D
+    ids, _ = D.shard_strong(total, rank, world, 42)
+    # a rollout-shaped tensor per env: [E_rank, 3, 5] float32 values that name their global env
+    g = torch.tensor(ids, dtype=torch.float32).reshape(-1, 1, 1)
+    mine = g * 100 + torch.arange(15, dtype=torch.float32).reshape(1, 3, 5)
+    full = D.gather_rollout(mine)
+    # an int tensor of one column too (dones-like), and an empty shard on the last rank
+    ints = D.gather_rollout(torch.tensor(ids, dtype=torch.int64))
+    out_q.put((rank, full.numpy(), ints.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total", [(2, 23), (3, 23), (3, 2)])
+def test_gather_rollout_unequal_shards(world, total):
+    """marl_gpu.dist.gather_rollout collates per-rank rollout tensors whose leading sizes differ
+    (shard_strong: 23 envs -> 12 + 11, 8 + 8 + 7; 2 envs over 3 ranks leaves one rank empty):
+    every rank gets the single-process tensor in global env order (MAPPO/trainer.py:172-286 stacks
+    every env's buffers for one learner)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = np.arange(total, dtype=np.float32).reshape(-1, 1, 1) * 100 + np.arange(15, dtype=np.float32).reshape(1, 3, 5)
+    for rank, full, ints in got:
+        np.testing.assert_array_equal(full, want, err_msg=f"rank {rank}")
+        np.testing.assert_array_equal(ints, np.arange(total))

@@ -76,7 +76,7 @@ def test_bench_plain_command_two_gpus_self_launches():
     command starts torch.distributed.run itself; the line says how many ranks the process group saw,
     which devices they ran on, and carries the CPU baseline (timed on rank 0 after the timed region)."""
     d = _plain(["--gpus", "2", "--backend", "gloo", "--steps", "40", "--warmup", "5", "--cpu-seconds", "1",
-                "--fused-k", "0"])
+                "--fused-k", "0", "--gather"])
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["launcher"] == "self"
     assert d["process_group_backend"] == "gloo"
     assert sorted(x["rank"] for x in d["devices"]) == [0, 1] and all("gfx950" in x["arch"] for x in d["devices"])
@@ -88,6 +88,21 @@ def test_bench_plain_command_two_gpus_self_launches():
     # the launch floor beside the step: an empty kernel in the step's launch shape
     assert 0 < d["launch_floor_ms_per_step"] and d["over_floor_us"] == pytest.approx(
         (d["ms_per_step"] - d["launch_floor_ms_per_step"]) * 1e3)
+    # the metric's own workload at N ranks -- 4,096 envs in TOTAL split over them --
+    # as a second timed region beside the weak one, and the reference's CPU figures, labelled
+    s = d["strong_4096"]
+    assert s["total_envs"] == 4096 and s["envs_per_rank"] == [2048, 2048] and s["scaling"] == "strong"
+    assert s["value"] == pytest.approx(4096 * 5 * s["steps"] / (s["ms_per_step"] * s["steps"] / 1e3), rel=1e-9)
+    assert s["launch_floor_ms_per_step"] > 0 and s["step_layout"] == "wave"
+    rc = d["reference_cpu"]
+    assert rc["serial_1core"] == 195453.0 and rc["processes_8"] == 1650597.0 and "BASELINE.md" in rc["source"]
+    # the optional rollout gather leg (gloo here: a rehearsal through host memory)
+    g = d["rollout_gather"]
+    assert g["gathered_bytes"] == 2 * 4096 * 1301 * 4 and g["bytes_per_rank"] == 4096 * 1301 * 4
+    assert g["ms_per_gather"] > 0 and g["backend"] == "gloo"
+    # the kernel label and layout come from the engine (mdl_step_kernel_name / mdl_last_step_layout)
+    assert d["roofline"]["kernel"] == "mdl::k_step<true, 1, false, 5>"
+    assert d["config"]["step_layout"].startswith("wave")
 
 
 def test_bench_one_gpu_launch_floor_and_config3_leg():

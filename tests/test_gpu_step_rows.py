@@ -2,8 +2,9 @@
 one-env-per-wavefront step (k_step, "wave"): same seeds, same actions, every output and the whole
 engine state (save_state: robots, packages, statuses, tracker, per-env scalars and reward-term bits,
 RNG words, episode records) bit for bit after every step -- across auto-resets, in both tracker
-modes, both action formats, A < 5 / A = 5 / A = 8 (numpy's 8-partial sum), P from 1 to 64 (four or eight package chunks per lane), env counts that leave the last
-wave's rows empty, and mixed maps.
+modes, both action formats, A < 5 / A = 5 / A = 8 (numpy's 8-partial sum), P from 1 to 64 (the four package chunks per lane of the
+only instantiated form, k_step_rows<.., .., 4>), env counts that leave the last wave's rows empty, mixed
+maps, and a done env stepped on without reset past t = 0xffff (the sentinel slots' start time).
 The oracle and golden-fixture tests run this kernel too (test_gpu_parity.py: test_vs_oracle_rows_layout,
 the "rows" cases of test_vs_oracle_map1 and test_mappo_rollout_golden); the default layout ("auto")
 picks it for full-batch steps of >= 7,168 envs (test_rows_auto_threshold)."""
@@ -123,15 +124,66 @@ def test_rows_auto_threshold():
     mg = _mg()
     small = mg.BatchedEnv(grid("map1.txt"), 7167, 5, 50, 30, seed=1)
     big = mg.BatchedEnv(grid("map1.txt"), 7168, 5, 50, 30, seed=1)
-    assert not small.step_rows and big.step_rows
+    # the engine's own decision (mdl_step_layout), and what its launches recorded (mdl_last_step_layout)
+    assert small.step_layout() == "wave" and big.step_layout() == "rows"
+    assert big.step_layout(n=7168) == "wave"   # an env_ids subset: always one wave per env
+    assert big.last_step_layout() is None
+    assert big.step_kernel_name() == "mdl::k_step_rows<true, 5, 4>"
+    assert small.step_kernel_name() == "mdl::k_step<true, 1, false, 5>"
     ref = mg.BatchedEnv(grid("map1.txt"), 7168, 5, 50, 30, seed=1, step_layout="wave")
-    for e in (big, ref):
+    for e in (big, ref, small):
         e.reset()
+    small.step(torch.zeros((7167, 5), dtype=torch.uint8, device="cuda"))
+    assert small.last_step_layout() == "wave"
     gen = torch.Generator(device="cuda").manual_seed(12)
     for k in range(40):
         acts = torch.randint(0, 15, (7168, 5), dtype=torch.uint8, device="cuda", generator=gen)
         r1, s1, d1 = big.step(acts)
+        assert big.last_step_layout() == "rows"
         r2, s2, d2 = ref.step(acts)
+        assert ref.last_step_layout() == "wave"
         assert torch.equal(r1, r2) and torch.equal(s1.view(torch.int32), s2.view(torch.int32)) and torch.equal(d1, d2)
+    big.step(torch.zeros((3, 5), dtype=torch.uint8, device="cuda"), env_ids=[0, 5, 9])
+    assert big.last_step_layout() == "wave"
+    ref.step(torch.zeros((3, 5), dtype=torch.uint8, device="cuda"), env_ids=[0, 5, 9])
     torch.cuda.synchronize()
     assert np.array_equal(big.save_state(), ref.save_state())
+
+
+def _set_clock(env, t):
+    """Every env's clock = t, through the checkpoint blob (header, then the state sections in
+    mdl_save_state's order: robots, packages, state words, env records {t, rterms, total})."""
+    E, A, P = env.E, env.A, env.P
+    blob = env.save_state()
+    pay = E * A * 4 + E * P * 8 + E * P * 2 + E * 16 + E * 624 * 4 + E * 4 + (E * P * 8 if env.tracker != "fresh"
+                                                                                  else 0) + E * 8 + E * 4
+    off = blob.nbytes - pay + E * A * 4 + E * P * 8 + E * P * 2
+    es = blob[off:off + E * 16].view(np.uint32).reshape(E, 4)
+    es[:, 0] = t
+    env.load_state(blob)
+
+
+@pytest.mark.parametrize("tracker", ["mappo", "fresh"])
+def test_rows_sentinel_slots_past_t_65535(tracker):
+    """slots without a package (j >= P) carry the sentinel start time 0xffff, so
+    a done env stepped on without reset reaches t1 == 0xffff and "spawns" them.  Their state-word
+    and tracker stores must stay off: the offsets of those slots name the next env's packages (or
+    lie past the allocation for the last env).  Both layouts from the same state near the wrap, 12
+    steps without reset: every output and the whole saved state equal, bit for bit."""
+    a, b = _pair(grid("map1.txt"), 8, 5, 20, 4, seed=17, tracker=tracker)
+    _run(a, b, 3, seed=2)
+    for e in (a, b):
+        _set_clock(e, 65530)
+    assert np.array_equal(a.save_state(), b.save_state())
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    for k in range(12):
+        acts = torch.randint(0, 15, (8, 5), dtype=torch.uint8, device="cuda", generator=gen)
+        r1, s1, d1 = a.step(acts, auto_reset=False)
+        r2, s2, d2 = b.step(acts, auto_reset=False)
+        assert b.last_step_layout() == "rows"
+        torch.cuda.synchronize()
+        assert torch.equal(r1, r2) and torch.equal(s1.view(torch.int32), s2.view(torch.int32)) and torch.equal(d1, d2)
+        assert np.array_equal(a.save_state(), b.save_state()), f"state differs after step {k} (t = {65531 + k})"
+    st = b.read_state()
+    torch.cuda.synchronize()
+    assert (st["t"].cpu().numpy() == 65542).all()

@@ -95,7 +95,7 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="eager launches only (PMC profiling passes)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend under torchrun (gloo: rehearse N ranks on fewer GPUs)")
-    ap.add_argument("--step-layout", default="auto", choices=("auto", "wave", "rows"),
+    ap.add_argument("--step-layout", default="auto", choices=("auto", "wave", "rows", "halves"),
                     help="mdl_step's env-to-wavefront mapping (MdlConfig.step_layout; same results): auto = four "
                          "envs per wavefront where A <= 8 and P <= 64")
     ap.add_argument("--host-wait", default="auto", choices=("auto", "spin", "yield", "blocking"),
@@ -613,8 +613,8 @@ def main(argv=None):
                        "obs_dims": ({"actor_vec": env.actor_vec_dim, "critic_vec": env.critic_vec_dim,
                                      "obs_bytes_per_env_step": obs_bytes_env} if obs_cfg else None),
                        "parallelism": f"env-shard x{world}",
-                       "step_layout": ("rows (4 envs per wavefront)" if layout == "rows"
-                                       else "wave (1 env per wavefront)"),
+                       "step_layout": {"rows": "rows (4 envs per wavefront)", "halves": "halves (2 envs per wavefront)"}
+                                      .get(layout, "wave (1 env per wavefront)"),
                        "step_layout_source": "engine (mdl_last_step_layout of the timed launches)"},
             "gpu_event_ms_per_step": gpu_ms / K,
             "eager": None if wall_eager is None else {"value": total_agent_steps / wall_eager,

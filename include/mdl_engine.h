@@ -68,14 +68,17 @@ typedef struct {
 #define MDL_OBS_BUILDER_GENERIC 1
 
 /* MdlConfig.step_layout.  ROWS: a full-batch mdl_step (env_ids NULL) runs four envs per wavefront,
- * one per 16-lane row (A <= 8, P <= 64; mdl_create fails otherwise).  WAVE: one env per wavefront
- * always.  AUTO: ROWS where it applies and the batch has at least 7,168 envs (where it is the
- * faster of the two on MI355X), WAVE otherwise.  Subset steps (env_ids), mdl_step_fused,
- * mdl_step_obs and the mailbox step always use one wave per env.  Every layout produces the same
- * state and outputs; WAVE / ROWS exist so tests can compare the two on one configuration. */
+ * one per 16-lane row (A <= 8, P <= 64; mdl_create fails otherwise).  HALVES: two envs per
+ * wavefront, one per 32-lane half (A == 16, P <= 128).  WAVE: one env per wavefront always.  AUTO:
+ * ROWS where it applies and the batch has at least 7,168 envs, HALVES where it applies and is the
+ * faster layout (see MdlEngine::HALVES_MIN_ENVS), WAVE otherwise.  Subset steps (env_ids),
+ * mdl_step_fused, mdl_step_obs and the mailbox step always use one wave per env.  Every layout
+ * produces the same state and outputs; the explicit layouts exist so tests can compare them on one
+ * configuration. */
 #define MDL_STEP_LAYOUT_AUTO 0
 #define MDL_STEP_LAYOUT_WAVE 1
 #define MDL_STEP_LAYOUT_ROWS 2
+#define MDL_STEP_LAYOUT_HALVES 3
 
 /* Create an engine on `device`.  grids: n_maps row-major 0/1 maps packed back
  * to back; map_hw: 2*n_maps (H, W); env_map: E map indices (NULL = all map 0).
@@ -337,14 +340,14 @@ int mdl_rank_table(int32_t H, int32_t W, uint16_t* out);
 
 /* Introspection */
 int mdl_get_config(const MdlEngine* eng, MdlConfig* out);
-/* The step layout (MDL_STEP_LAYOUT_WAVE or _ROWS) mdl_step launches for a call over n envs
+/* The step layout (MDL_STEP_LAYOUT_WAVE, _ROWS or _HALVES) mdl_step launches for a call over n envs
  * (use_ids = 0: the full batch, n ignored as in mdl_step; use_ids = 1: an env_ids subset of n,
  * always WAVE) -- the engine's own decision, the one mdl_step takes. */
 int mdl_step_layout(const MdlEngine* eng, int32_t n, int32_t use_ids, int32_t* layout);
 /* The layout of the last mdl_step launch on this engine (0 before the first one). */
 int mdl_last_step_layout(const MdlEngine* eng, int32_t* layout);
 /* The symbol (as rocprof reports it, e.g. "mdl::k_step<true, 1, false, 5>") of the kernel mdl_step
- * launches in `layout` (WAVE / ROWS), or, with with_obs, of mdl_step_obs's step launch (its fused
+ * launches in `layout` (WAVE / ROWS / HALVES), or, with with_obs, of mdl_step_obs's step launch (its fused
  * step + observation kernel where it applies).  NUL-terminated into out[cap]. */
 int mdl_step_kernel_name(const MdlEngine* eng, int32_t layout, int32_t with_obs, char* out, int32_t cap);
 int mdl_obs_dims(const MdlEngine* eng, int32_t* actor_vec_dim, int32_t* critic_vec_dim);

@@ -121,6 +121,9 @@ struct MdlEngine {
     bool step_rows = false;   // k_step_rows applies (A <= 8, P <= 64) and the layout allows it
     bool rows_forced = false; // MDL_STEP_LAYOUT_ROWS: at every batch size
     size_t lds_rows = 0;
+    bool step_halves = false;   // k_step_halves applies (A == 16, P <= 128) and the layout allows it
+    bool halves_forced = false; // MDL_STEP_LAYOUT_HALVES: at every batch size
+    size_t lds_halves = 0;
     // Whether a full-batch step over n envs runs four envs per wavefront.  AUTO: from ROWS_MIN_ENVS
     // envs on.  Below that the step is latency bound -- one wave's dependent chain is longer for
     // k_step_rows, whose wave does four envs' work -- and one wave per env wins (4,096 envs: 4.19
@@ -129,8 +132,19 @@ struct MdlEngine {
     // config 4's 65,536 28.7 vs 21.1; profiles/r05/rows_ab.txt).
     static constexpr int ROWS_MIN_ENVS = 7168;
     bool rows_for(int n) const { return step_rows && (rows_forced || n >= ROWS_MIN_ENVS); }
+    // Two envs per wavefront (k_step_halves) from HALVES_MIN_ENVS envs on (AUTO).
+    static constexpr int HALVES_MIN_ENVS = 1 << 30;   // not chosen by AUTO until measured
+    bool halves_for(int n) const { return step_halves && (halves_forced || n >= HALVES_MIN_ENVS); }
     // the layout mdl_step launches for a call over n envs (with an id list: always one wave per env)
-    int32_t layout_for(int n, bool ids) const { return (!ids && rows_for(n)) ? MDL_STEP_LAYOUT_ROWS : MDL_STEP_LAYOUT_WAVE; }
+    int32_t layout_for(int n, bool ids) const {
+        if (ids) return MDL_STEP_LAYOUT_WAVE;
+        if (rows_for(n)) return MDL_STEP_LAYOUT_ROWS;
+        if (halves_for(n)) return MDL_STEP_LAYOUT_HALVES;
+        return MDL_STEP_LAYOUT_WAVE;
+    }
+    size_t lds_for(int32_t layout) const {
+        return layout == MDL_STEP_LAYOUT_ROWS ? lds_rows : layout == MDL_STEP_LAYOUT_HALVES ? lds_halves : lds_step;
+    }
     int32_t last_step_layout = 0;   // MDL_STEP_LAYOUT_* of the last mdl_step launch (0: none yet)
     // A synchronous host-mapped call whose wait timed out leaves its launch queued on `hung`: until that
     // stream has drained, no call may rewrite the mailbox / arena inputs that launch still reads.
@@ -452,13 +466,19 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     eng->lds_step = mdl::step_lds((int)P);
     eng->wpb_step = waves_per_block(eng->lds_step);
     if (c.step_layout != MDL_STEP_LAYOUT_AUTO && c.step_layout != MDL_STEP_LAYOUT_WAVE &&
-        c.step_layout != MDL_STEP_LAYOUT_ROWS)
+        c.step_layout != MDL_STEP_LAYOUT_ROWS && c.step_layout != MDL_STEP_LAYOUT_HALVES)
         return fail("unknown step_layout %d", c.step_layout);
     if (c.step_layout == MDL_STEP_LAYOUT_ROWS && !mdl::step_rows_ok((int)A, (int)P))
         return fail("step_layout ROWS needs A <= 8 and P <= 64 (A=%d P=%d)", (int)A, (int)P);
-    eng->step_rows = c.step_layout != MDL_STEP_LAYOUT_WAVE && mdl::step_rows_ok((int)A, (int)P);
+    if (c.step_layout == MDL_STEP_LAYOUT_HALVES && !mdl::step_halves_ok((int)A, (int)P))
+        return fail("step_layout HALVES needs A == 16 and P <= 128 (A=%d P=%d)", (int)A, (int)P);
+    const bool auto_l = c.step_layout == MDL_STEP_LAYOUT_AUTO;
+    eng->step_rows = (auto_l || c.step_layout == MDL_STEP_LAYOUT_ROWS) && mdl::step_rows_ok((int)A, (int)P);
     eng->rows_forced = c.step_layout == MDL_STEP_LAYOUT_ROWS;
     eng->lds_rows = mdl::step_rows_lds((int)P);
+    eng->step_halves = (auto_l || c.step_layout == MDL_STEP_LAYOUT_HALVES) && mdl::step_halves_ok((int)A, (int)P);
+    eng->halves_forced = c.step_layout == MDL_STEP_LAYOUT_HALVES;
+    eng->lds_halves = mdl::step_halves_lds((int)P);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) eng->n_cu = prop.multiProcessorCount;
@@ -554,6 +574,12 @@ int mdl_step(MdlEngine* eng, const uint8_t* actions, int32_t action_format, cons
                                      (hipStream_t)stream));
         return 0;
     }
+    if (layout == MDL_STEP_LAYOUT_HALVES) {
+        HIPCHK(mdl::launch_step_halves(eng->p, actions, action_format, n, auto_reset, r_env, r_shaped, done,
+                                       step_wpb(n, eng->n_cu, eng->lds_halves, eng->p.P), eng->lds_halves,
+                                       (hipStream_t)stream));
+        return 0;
+    }
     HIPCHK(mdl::launch_step(eng->p, actions, action_format, env_ids, n, auto_reset, r_env, r_shaped, done,
                             step_wpb(n, eng->n_cu, eng->lds_step, eng->p.P), eng->lds_step, (hipStream_t)stream));
     return 0;
@@ -563,10 +589,11 @@ int mdl_step_floor(MdlEngine* eng, int32_t n, void* stream) {
     if (!eng) return fail("mdl_step_floor: null engine");
     if (n < 1 || n > eng->p.E) return fail("mdl_step_floor: n=%d out of range", n);
     DeviceGuard dg(eng->device);
-    // the launch shape of a full-batch mdl_step over n envs (the rows grid when that layout is on)
-    const bool rows = eng->rows_for(n);
-    const size_t lds = rows ? eng->lds_rows : eng->lds_step;
-    HIPCHK(mdl::launch_step_floor(eng->p, n, step_wpb(n, eng->n_cu, lds, eng->p.P), lds, (hipStream_t)stream, rows));
+    // the launch shape of a full-batch mdl_step over n envs (the layout mdl_step takes for it)
+    const int32_t layout = eng->layout_for(n, false);
+    const size_t lds = eng->lds_for(layout);
+    const int epw = layout == MDL_STEP_LAYOUT_ROWS ? 4 : layout == MDL_STEP_LAYOUT_HALVES ? 2 : 1;
+    HIPCHK(mdl::launch_step_floor(eng->p, n, step_wpb(n, eng->n_cu, lds, eng->p.P), lds, (hipStream_t)stream, epw));
     return 0;
 }
 
@@ -1212,14 +1239,16 @@ int mdl_step_layout(const MdlEngine* eng, int32_t n, int32_t use_ids, int32_t* l
 
 int mdl_step_kernel_name(const MdlEngine* eng, int32_t layout, int32_t with_obs, char* out, int32_t cap) {
     if (!eng || !out || cap < 1) return fail("mdl_step_kernel_name: bad argument");
-    if (layout != MDL_STEP_LAYOUT_WAVE && layout != MDL_STEP_LAYOUT_ROWS)
-        return fail("mdl_step_kernel_name: layout %d is not WAVE or ROWS", layout);
-    if (layout == MDL_STEP_LAYOUT_ROWS && (with_obs || !eng->step_rows))
-        return fail("mdl_step_kernel_name: no rows-layout launch in this configuration");
+    if (layout != MDL_STEP_LAYOUT_WAVE && layout != MDL_STEP_LAYOUT_ROWS && layout != MDL_STEP_LAYOUT_HALVES)
+        return fail("mdl_step_kernel_name: layout %d is not WAVE, ROWS or HALVES", layout);
+    if ((layout == MDL_STEP_LAYOUT_ROWS && (with_obs || !eng->step_rows)) ||
+        (layout == MDL_STEP_LAYOUT_HALVES && (with_obs || !eng->step_halves)))
+        return fail("mdl_step_kernel_name: no launch in layout %d in this configuration", layout);
     // mdl_step_obs's one-launch form (else it is mdl_step's wave kernel + the builder)
     const bool obs = with_obs && eng->p.obs_small && eng->p.A <= 8 && eng->p.P <= 64 &&
                      std::max(eng->lds_step, eng->lds_obs) <= LDS_BUDGET;
-    const int k = mdl::step_kernel_name(eng->p, layout == MDL_STEP_LAYOUT_ROWS, obs, out, cap);
+    const int epw = layout == MDL_STEP_LAYOUT_ROWS ? 4 : layout == MDL_STEP_LAYOUT_HALVES ? 2 : 1;
+    const int k = mdl::step_kernel_name(eng->p, epw, obs, out, cap);
     if (k < 0 || k >= cap) return fail("mdl_step_kernel_name: buffer of %d bytes too small", cap);
     return 0;
 }

@@ -1187,6 +1187,7 @@ __global__ __launch_bounds__(256) MDL_STEP_ATTR(1, false) void k_step_obs(const 
 }
 
 #include "mdl_step_rows.hpp"
+#include "mdl_step_halves.hpp"
 
 // ------------------------------------------------------------- observations
 // Tracker slots staged in LDS for the feature builders (random access by id).
@@ -1805,6 +1806,41 @@ size_t step_rows_lds(int P) {
     return a > b ? a : b;
 }
 
+// A == 16 exactly (numpy's pairwise sum of 16 values in-row; 9..15 would need its sequential
+// tail), P <= 128 (four 32-lane chunks)
+bool step_halves_ok(int A, int P) { return A == 16 && P >= 1 && P <= HALF * HALF_NC; }
+size_t step_halves_lds(int P) {
+    const size_t a = reset_lds_bytes(P), b = halves_scratch_bytes();
+    return a > b ? a : b;
+}
+
+hipError_t launch_step_halves(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
+                              float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
+    if (!step_halves_ok(p.A, p.P)) return hipErrorInvalidValue;
+    StepArgs a;
+    a.p = p;
+    a.actions = actions;
+    a.env_ids = nullptr;
+    a.r_out = r;
+    a.sh_out = sh;
+    a.done_out = done;
+    a.fmt = fmt;
+    a.n = n;
+    a.auto_reset = auto_reset;
+    a.wpb = wpb;
+    a.lds_stride = (int)lds;
+    a.K = 1;
+    const int waves = (n + 1) / 2;
+    const dim3 grid(blocks_for(waves, wpb)), block(64 * wpb);
+    const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
+    const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
+#define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a
+    if (p.stale) hipLaunchKernelGGL((k_step_halves<true>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    else hipLaunchKernelGGL((k_step_halves<false>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+#undef MDL_STEP_ARGS
+    return hipGetLastError();
+}
+
 hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
                             float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s) {
     if (!step_rows_ok(p.A, p.P)) return hipErrorInvalidValue;
@@ -1838,24 +1874,25 @@ hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt,
     return hipGetLastError();
 }
 
-// (the dispatch of launch_step_rows above, launch_step_obs and launch_step_t below)
-int step_kernel_name(const DevParams& p, bool rows, bool obs, char* out, int cap) {
+// (the dispatch of launch_step_rows / launch_step_halves above, launch_step_obs and launch_step_t below)
+int step_kernel_name(const DevParams& p, int envs_per_wave, bool obs, char* out, int cap) {
     const char* st = p.stale ? "true" : "false";
-    if (rows) return snprintf(out, (size_t)cap, "mdl::k_step_rows<%s, %d, 4>", st, p.A == 5 ? 5 : 8);
+    if (envs_per_wave == 4) return snprintf(out, (size_t)cap, "mdl::k_step_rows<%s, %d, 4>", st, p.A == 5 ? 5 : 8);
+    if (envs_per_wave == 2) return snprintf(out, (size_t)cap, "mdl::k_step_halves<%s>", st);
     if (obs) return snprintf(out, (size_t)cap, "mdl::k_step_obs<%s, %d>", st, p.A == 5 ? 5 : 8);
     const int nch = nch_for(p.P);
     const int au = (nch <= 2 && p.A == 5) ? 5 : (nch <= 2 && p.A == 16) ? 16 : p.A <= 8 ? 8 : 0;
     return snprintf(out, (size_t)cap, "mdl::k_step<%s, %d, false, %d>", st, nch, au);
 }
 
-hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s, bool rows) {
+hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s, int envs_per_wave) {
     StepArgs a{};
     a.p = p;
     a.n = n;
     a.wpb = wpb;
     a.lds_stride = (int)lds;
     a.K = 1;
-    const dim3 grid(blocks_for(rows ? (n + 3) / 4 : n, wpb)), block(64 * wpb);
+    const dim3 grid(blocks_for((n + envs_per_wave - 1) / envs_per_wave, wpb)), block(64 * wpb);
     const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
     hipLaunchKernelGGL(k_step_floor, grid, block, lds * wpb, s, p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk,

@@ -19,16 +19,23 @@ hipError_t launch_step(const DevParams& p, const uint8_t* actions, int fmt, cons
 // k_step_rows (mdl_step_rows.hpp): a full-batch step with four envs per wavefront, one per 16-lane
 // row; A <= 8, P <= 64 (step_rows_ok).  lds: the per-wave slice (step_rows_lds).
 bool step_rows_ok(int A, int P);
-// The symbol (as rocprof names it) of the step kernel a launch takes: launch_step_rows (rows),
-// launch_step_obs (obs: the fused step + observation kernel) or launch_step.  Mirrors their
-// dispatch; bench.py labels its roofline record with it.  Returns snprintf's count.
-int step_kernel_name(const DevParams& p, bool rows, bool obs, char* out, int cap);
+// The symbol (as rocprof names it) of the step kernel a launch takes: launch_step_rows
+// (envs_per_wave 4), launch_step_halves (2), launch_step_obs (obs: the fused step + observation
+// kernel) or launch_step (1).  Mirrors their dispatch; bench.py labels its roofline record with it.
+// Returns snprintf's count.
+int step_kernel_name(const DevParams& p, int envs_per_wave, bool obs, char* out, int cap);
 size_t step_rows_lds(int P);
+// k_step_halves (mdl_step_halves.hpp): a full-batch step with two envs per wavefront, one per 32-lane
+// half; A == 16, P <= 128 (step_halves_ok).  lds: the per-wave slice (step_halves_lds).
+bool step_halves_ok(int A, int P);
+size_t step_halves_lds(int P);
+hipError_t launch_step_halves(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
+                              float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s);
 hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt, int n, int auto_reset, double* r,
                             float* sh, uint8_t* done, int wpb, size_t lds, hipStream_t s);
 // the step's launch shape (grid, workgroup, LDS, kernel arguments) with an empty kernel; rows: the
-// k_step_rows grid (four envs per wave)
-hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s, bool rows = false);
+// grid of the layout's envs per wave (1: k_step, 2: k_step_halves, 4: k_step_rows)
+hipError_t launch_step_floor(const DevParams& p, int n, int wpb, size_t lds, hipStream_t s, int envs_per_wave = 1);
 hipError_t launch_step_fused(const DevParams& p, const uint8_t* actions, int fmt, const int* ids, int n, int K,
                              int auto_reset, double* r, float* sh, uint8_t* done, int wpb, size_t lds,
                              hipStream_t s);

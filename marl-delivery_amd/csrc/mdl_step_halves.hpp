@@ -1,0 +1,520 @@
+// mdl_step_halves.hpp -- the step kernel with TWO ENVS PER WAVEFRONT, one per 32-lane half, for
+// the eight-to-sixteen-robot configurations (8 <= A <= 16, P <= 128: BASELINE config 5's 16 robots
+// and 100 packages).  Included by mdl_kernels.hip after mdl_step_rows.hpp; same reference semantics
+// (env.py:173-316, MAPPO/helper.py:257-369, MAPPO/trainer.py:95-130,211-259).
+//
+// Why: k_step<.., 16> runs one env per wave and is issue bound at config 5's 131,072 envs (~395
+// VALU + ~264 SALU per wave at 128 waves per SIMD; profiles/r05 prices each wave instruction at ~3
+// cycles per SIMD there).  Its scalar work (prologue, loop control, exec handling, ballots and
+// their SALU follow-up) and every cross-lane operation serve one env.  Here env h of the wave lives
+// on lanes 32h..32h+31:
+//   * robot a on lanes 32h + a AND 32h + 16 + a (both 16-lane rows of the half hold every robot and
+//     compute the same robot values, so a robot's data is a row-local DPP broadcast away from every
+//     lane of its half, and no value has to cross the rows);
+//   * package j on half-lane j & 31 of chunk j >> 5 (NC = 4 chunks, P <= 128);
+//   * a minimum over the half is four in-row DPP stages plus one v_permlane16_swap (rows 0 <-> 1,
+//     2 <-> 3) and a min.
+// Every scalar instruction and every ballot serves both envs.  The shaped reward's nearest waiting
+// package keeps k_step's compacted candidate scan, per half: each half packs its waiting candidates
+// into its own LDS list and the two rows of a half scan alternate candidates for the same agent.
+//
+// Scope: full-batch steps (no env_ids), one step per launch; k_step stays for everything else.
+// Results are bit-identical to k_step's (tests/test_gpu_step_halves.py steps both layouts side by
+// side and compares every output and the whole saved state).
+#pragma once
+
+constexpr int HALF = 32;                 // lanes per env
+constexpr int HALF_NC = 4;               // package chunks per lane: P <= 128
+constexpr int HALF_CAND = 136;           // candidate slots per half (<= 128 candidates, padded to a multiple of 4)
+
+// minimum over the 32 lanes of this lane's half, on every lane of the half
+__device__ __forceinline__ uint32_t half_min_u32(uint32_t m) {
+    m = row_min_u32(m);
+    const auto r = __builtin_amdgcn_permlane16_swap(m, m, false, false);   // [r0, r0, r2, r2], [r1, r1, r3, r3]
+    return r[0] < r[1] ? r[0] : r[1];
+}
+
+// LDS bytes per wave: the carried-package gather records (4 chunks x 64 lanes x 16 B), the flag bytes
+// (64 lanes x 4), the two halves' candidate lists; the reset scratch reuses the slice.
+__host__ __device__ constexpr size_t halves_scratch_bytes() {
+    return (size_t)HALF_NC * 64 * 16 + 64 * (size_t)HALF_NC + 2 * (size_t)HALF_CAND * 8;
+}
+
+template <bool STALE>
+__global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict__ rob_pre,
+                                                     const uint64_t* __restrict__ pkg_pre,
+                                                     const uint16_t* __restrict__ pst_pre,
+                                                     const u32x4* __restrict__ es_pre,
+                                                     const uint64_t* __restrict__ trk_pre,
+                                                     const uint8_t* __restrict__ act_pre, uint32_t ap, uint32_t nw,
+                                                     StepArgs args) {
+    constexpr int NC = HALF_NC;
+    constexpr uint32_t NONE = 255u;   // no package slot (slots < 128)
+    extern __shared__ __align__(16) unsigned char smem[];
+    const DevParams& p = args.p;
+    const int A = (int)(ap & 0x7fu), P = (int)((ap >> 7) & 0x7ffu);
+    const int n_ = (int)(nw & 0xffffffu), wpb_ = (int)((nw >> 24) & 31u);
+    GLOBAL const uint32_t* robp = (GLOBAL const uint32_t*)rob_pre;
+    GLOBAL const uint64_t* pkgp = (GLOBAL const uint64_t*)pkg_pre;
+    GLOBAL const uint16_t* pstp = (GLOBAL const uint16_t*)pst_pre;
+    GLOBAL const u32x4* esp = (GLOBAL const u32x4*)es_pre;
+    GLOBAL const uint64_t* trkp = (GLOBAL const uint64_t*)trk_pre;
+    GLOBAL const uint8_t* actp = (GLOBAL const uint8_t*)act_pre;
+
+    const int wave = wave_id();
+    const int lane = lane_id();
+    const int nbp = (int)(ap >> AP_NB_SHIFT);
+    const int w = (nbp ? xcd_slot((int)blockIdx.x, nbp) : (int)blockIdx.x) * wpb_ + wave;
+    const int e0 = 2 * w;   // this wave's envs: e0, e0 + 1
+    if (wave >= wpb_ || e0 >= n_) return;
+    const int h = lane >> 5, hl = lane & 31, hbase = lane & 32, rbase = lane & 48;
+    const int ri = lane & 15;                // the robot this lane holds (on both rows of the half)
+    const bool live = e0 + h < n_;           // the last wave's second half past n holds no env
+    const bool act = live && ri < A;
+    const bool row0 = (lane & 16) == 0;      // the robot copy that stores
+
+    // ---- loads: one round trip, every lane loads (in-bounds offsets, discarded where unused) ----
+    const uint32_t roff = (uint32_t)(h * A + ri);
+    const uint32_t roff_c = (act ? roff : 0u) & 0x1fu;   // h * A + ri < 32
+    const uint32_t rv_ld = (robp + (size_t)e0 * A)[roff_c];
+    const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
+    uint64_t pk[NC], td[NC];
+    uint32_t ps[NC], ps_in[NC], tq[NC];
+    bool dirty[NC], pv[NC];
+    GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
+    GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
+    GLOBAL const uint64_t* trke = trkp + (size_t)e0 * P;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const int j = c * HALF + hl;
+        pv[c] = live && j < P;
+        const uint32_t o = (pv[c] ? (uint32_t)(h * P + j) : 0u) & 0xffu;   // h * P + j < 256
+        pk[c] = pkge[o];
+        ps[c] = pste[o];
+        td[c] = STALE ? trke[o] : 0ull;
+        dirty[c] = false;
+    }
+    const uint32_t erow = (uint32_t)(live ? h : 0) & 1u;
+    const uint32_t t_ld = ((GLOBAL const uint32_t*)(esp + e0))[4u * erow];
+    const uint64_t tot_ld = ((GLOBAL const uint64_t*)(esp + e0))[2u * erow + 1u];
+    KargPtr kap = (KargPtr)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                            offsetof(StepKarg, args));
+    const double cst = kap->p.cost_fold[hl];   // cost_fold[k] on half-lane k (n_cost <= 16)
+    __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any use
+    const uint32_t rv = act ? rv_ld : 0u;
+    int araw = act ? (int)(ar_ld & 0xffu) : 0;
+    const uint32_t t_rec = live ? t_ld : 0u;
+    const uint64_t tot_rec = live ? tot_ld : 0ull;
+    // slots without a package: the sentinels of k_step_rows (status delivered, start time and
+    // start cell 0xffff); every store below tests pv
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        pk[c] = pv[c] ? pk[c] : ~0ull;
+        ps[c] = pv[c] ? ps[c] : (uint32_t)ST_DELIVERED;
+        td[c] = pv[c] ? td[c] : ~0ull;
+        ps_in[c] = ps[c];
+    }
+    const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride;
+    const int T = p.T;
+    unsigned char* slice = smem + (size_t)wave * lds_stride;
+    int mvoff = p.maps[0].mvc_off;
+    int mi = 0;
+    if (nw & NW_MAP) {   // mixed maps: each half's map
+        mi = (int)((GLOBAL const uint8_t*)p.env_map)[e0 + (live ? h : 0)];
+#pragma unroll
+        for (int k = 1; k < MAX_MAPS; k++) mvoff = (mi == k) ? p.maps[k].mvc_off : mvoff;
+    }
+    int cell = rob_cell(rv), carry = rob_carry(rv);
+    uint32_t vmask = rob_valid(rv);
+    const int t0 = (int)t_rec;
+    const double tot_cur = __hiloint2double((int)(uint32_t)(tot_rec >> 32), (int)(uint32_t)tot_rec);
+
+    int mv, op;
+    decode_action(araw, fmt, mv, op);
+    mv = act ? mv : MV_S;
+    op = act ? op : 0;
+    uint32_t ps0[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const int j = c * HALF + hl;
+        ps0[c] = ps[c];
+        if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
+            td[c] = pk[c];
+            tq[c] = STALE ? ORD_EPISODE + (uint32_t)j : (uint32_t)j;
+        } else {
+            tq[c] = ps0[c] >> PS_RANK_SHIFT;
+        }
+    }
+
+    // ---- the shaped reward's candidates (tracker_prev's waiting entries with st <= t): pre-step
+    // state only, packed now into each half's LDS list {start cell, order key << 10 | slot} ----
+    int stc[NC];
+    uint64_t anyw = 0, wvm[NC];
+    bool wv[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const uint32_t f = ps0[c];
+        const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
+        wv[c] = waiting && pk_st(td[c]) <= t0;
+        stc[c] = pk_start(td[c]);
+        wvm[c] = ballot(wv[c]);
+        anyw |= wvm[c];
+    }
+    uint64_t* cand = (uint64_t*)(slice + NC * 64 * 16 + 64 * NC) + h * HALF_CAND;   // this lane's half
+    int nwg = 0;
+    if (anyw) {
+        const uint64_t hm = h ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+        const uint64_t lt = lanemask_lt() & hm;
+        int n0 = 0, n1 = 0, nh = 0;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int idx = nh + popc64(wvm[c] & lt);
+            const uint32_t klo = (tq[c] << 10) | (uint32_t)(c * HALF + hl);
+            if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo << 32);
+            n0 += popc64(wvm[c] & 0x00000000ffffffffull);
+            n1 += popc64(wvm[c] & 0xffffffff00000000ull);
+            nh = h ? n1 : n0;
+        }
+        // both halves scan the same (wave-uniform) count: each pads its list with sentinels (key bits
+        // ~0: never below a real key; cell ~0: no map cell) to a multiple of 4 of the longer one
+        nwg = (max(n0, n1) + 3) & ~3;
+        for (int k = nh + hl; k < nwg; k += HALF) cand[k] = ~0ull;
+    }
+
+    // ---- the pre-step carried package of each robot, through LDS; the flag bytes cleared ----
+    const int pj = carry - 1;
+    u32x4* grec = (u32x4*)slice;
+    unsigned char* flb = slice + NC * 64 * 16;   // byte (lane, c) <-> package slot c * 32 + (lane & 31) of the half
+#pragma unroll
+    for (int c = 0; c < NC; c++) grec[c * 64 + lane] = u32x4{ps0[c], tgt_dl(pk[c]), tgt_dl(td[c]), 0u};
+    ((uint32_t*)flb)[lane] = 0;
+    wave_sync();
+    const u32x4 g = grec[((pj >> 5) & (NC - 1)) * 64 + hbase + (pj & 31)];
+    const uint32_t g_pf = g.x, g_pk = g.y, g_td = g.z;
+
+    // ---- movement (env.py:188-257), row-local: every row holds its half's 16 robots ----
+    const int pcell = cell, pcarry = carry;
+    constexpr uint64_t DTAB = (uint64_t)(0x3ffu & (uint32_t)-256) << 10 | (uint64_t)256 << 20 |
+                              (uint64_t)(0x3ffu & (uint32_t)-1) << 30 | (uint64_t)1 << 40;
+    const int dtab = __builtin_amdgcn_sbfe((int)(uint32_t)(DTAB >> (10 * mv)), 0, 10);
+    const int vok = __builtin_amdgcn_sbfe((int)vmask, mv, 1);
+    const int prop = cell + (int)(lmask(act) & (uint32_t)(dtab & vok));
+    const bool mover = act && prop != cell;
+    const uint64_t movers = ballot(mover);
+    const uint32_t pvm = (uint32_t)(p.movevalid_cell + mvoff)[(uint32_t)prop];
+    uint64_t moved = 0;
+    if (movers) {
+        // one word per robot: its proposal if it moves (0xffff otherwise: a non-mover blocks nobody) |
+        // its cell << 16 (0xfffe where there is no robot)
+        const uint32_t wd = (mover ? (uint32_t)prop : 0xffffu) | ((act ? (uint32_t)cell : 0xfffeu) << 16);
+        uint32_t hit = 0;
+        int occ = -1;
+#define MDL_HMOV(J)                                                      \
+    {                                                                    \
+        const uint32_t wj = (uint32_t)row_bcast<J>((int)wd);             \
+        hit |= (wj & 0xffffu) == (uint32_t)prop ? (1u << J) : 0u;        \
+        occ = (wj >> 16) == (uint32_t)prop ? J : occ;                    \
+    }
+        MDL_HMOV(0) MDL_HMOV(1) MDL_HMOV(2) MDL_HMOV(3) MDL_HMOV(4) MDL_HMOV(5) MDL_HMOV(6) MDL_HMOV(7)
+        MDL_HMOV(8) MDL_HMOV(9) MDL_HMOV(10) MDL_HMOV(11) MDL_HMOV(12) MDL_HMOV(13) MDL_HMOV(14) MDL_HMOV(15)
+#undef MDL_HMOV
+        // a lower-index mover into the same cell (hit holds movers only)
+        const bool blocked = (hit & ((1u << ri) - 1u)) != 0u;
+        const uint32_t Mbase = lmask(mover && !blocked), Mfree = lmask(occ < 0);
+        moved = ballot((Mbase & Mfree) != 0u);
+        if (ballot((Mbase & ~Mfree) != 0u)) {   // some walk into an occupied cell: resolve the chains
+            const int oln = rbase + (occ & 15);
+            for (int it = 0; it < A; it++) {
+                const uint64_t nm = ballot((Mbase & (Mfree | vbit(moved, oln))) != 0u);
+                if (nm == moved) break;
+                moved = nm;
+            }
+        }
+        if ((moved >> lane) & 1ull) cell = prop;
+    }
+    const int n_cost = (int)__popc(row_bits(moved, rbase));
+
+    // ---- package actions (env.py:259-292) ----
+    // Pick-ups: each picking robot takes the lowest-index waiting package at its cell (robots sit on
+    // distinct cells, so the reference's robot order changes nothing).  Per robot index J, one
+    // minimum over the half's package slots answers robot J of both envs.
+    const bool picker = act && op == 1 && carry == 0;
+    const uint64_t pickers = ballot(picker);
+    int cnew = carry;
+    if (pickers) {
+        int sw[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) sw[c] = (ps[c] & PS_STATUS) == ST_WAITING ? pk_start(pk[c]) : -2;
+        for (uint32_t u = rows_union(pickers); u; u &= u - 1) {
+            const int J = __ffs((int)u) - 1;
+            const int ci = __builtin_amdgcn_ds_bpermute((rbase + J) << 2, cell);   // robot J's cell, row-local
+            uint32_t k = NONE;
+#pragma unroll
+            for (int c = NC - 1; c >= 0; c--) k = sw[c] == ci ? (uint32_t)(c * HALF + hl) : k;
+            k = half_min_u32(k);
+            cnew = (ri == J && picker && k != NONE) ? (int)k + 1 : cnew;
+        }
+    }
+    const bool picked = cnew != carry;
+    carry = cnew;
+    const int g_tgt = (int)(g_pk & 0xffffu), g_dl = (int)(g_pk >> 16);
+    const bool drop = act && op == 2 && carry != 0 && g_tgt == cell;
+    const uint64_t dmask = ballot(drop), omask = ballot(drop && t0 <= g_dl);
+    // one flag byte per package slot, written by the robot concerned (row 0's copy): the slot's new
+    // status (bits 0-1) | F_CHG | F_CARRY, as k_step_rows
+    constexpr uint32_t F_CHG = 8u, F_CARRY = 4u;
+    {
+        const int fs = drop ? pj : carry - 1;
+        const uint32_t fv = picked ? (F_CHG | F_CARRY | (uint32_t)ST_IN_TRANSIT)
+                            : drop ? (F_CHG | (uint32_t)ST_DELIVERED) : F_CARRY;
+        if (act && row0 && carry != 0) flb[(hbase + (fs & 31)) * NC + (fs >> 5)] = (unsigned char)fv;
+    }
+    carry = drop ? 0 : carry;
+    wave_sync();
+    const uint32_t fw = ((const uint32_t*)flb)[lane];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const uint32_t f = fw >> (8 * c);
+        const uint32_t clr = (0u - ((f >> 3) & 1u)) & PS_STATUS;
+        ps[c] = (ps[c] & ~clr) | (f & PS_STATUS);
+    }
+    // reward: fp64 fold in the reference's order (move costs, then deliveries in robot order)
+    double rr;
+    {
+        const int src = (hbase + n_cost) << 2;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)__double2loint(cst));
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)__double2hiint(cst));
+        rr = __hiloint2double((int)hi, (int)lo);
+    }
+    const uint32_t drow = row_bits(dmask, rbase), orow = row_bits(omask, rbase);
+    if (dmask) {
+        double DR = p.delivery_reward, DL = p.delay_reward;
+        pin(DR);
+        pin(DL);
+        for (uint32_t u = rows_union(dmask); u; u &= u - 1) {
+            const int i = __ffs((int)u) - 1;
+            const double add = ((orow >> i) & 1u) ? DR : DL;
+            rr = ((drow >> i) & 1u) ? rr + add : rr;
+        }
+    }
+    const uint32_t rfl = (n_cost ? RT_MOVE : 0u) | (orow ? RT_ONTIME : 0u) | ((drow & ~orow) ? RT_LATE : 0u);
+    const int t1 = t0 + 1;
+    const double total = tot_cur + rr;
+
+    // ---- terminate (env.py:308-316) + spawn (get_state env.py:133-137) ----
+    uint32_t undel = 0;
+    uint64_t spawned = 0;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        undel |= (ps[c] & PS_STATUS) ^ (uint32_t)ST_DELIVERED;
+        const bool sp = pk_st(pk[c]) == t1;
+        spawned |= ballot(sp);
+        ps[c] = sp ? ((ps[c] & ~PS_STATUS) | ST_WAITING) : ps[c];
+    }
+    const uint64_t und = ballot(undel != 0u);
+    const uint32_t alldel = lmask(((und >> hbase) & 0xffffffffull) == 0ull);
+    const bool done = (lmask(live) & (lmask(t1 == T) | alldel)) != 0u;
+
+    // ---- shaped reward with the pre-step tracker (MAPPO/helper.py:257-369) ----
+    float s_lane;
+    {
+        const uint32_t pf = g_pf;
+        const uint32_t Mact = lmask(act), Mpc0 = lmask(pcarry == 0), Mc0 = lmask(carry == 0);
+        const uint32_t Mpres =
+            Mact & ~Mpc0 & lmask(pcarry <= P) &
+            (STALE ? lmask((pf & PS_PRESENT) != 0)
+                   : lmask((pf & PS_STATUS) == ST_WAITING) | lmask((pf & PS_STATUS) == ST_IN_TRANSIT));
+        const uint32_t Mmov = lmask(pcell != cell), MS = lmask(mv == MV_S);
+        const uint32_t Mop1 = lmask(op == 1), Mop2 = lmask(op == 2);
+        uint32_t Midle = 0, Mcan = 0;
+        int best_cell = -1;
+        if (anyw) {
+            // The two rows of a half scan alternate candidates for the same agent (two per step, two
+            // LDS reads in flight): nearest key from the pre-step cell, and "a waiting package starts
+            // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.
+            const uint64_t* cp = cand + ((lane >> 4) & 1);
+            uint32_t kmin = 0xffffffffu;
+            uint64_t hmc = 0;
+            for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
+                const uint64_t ce = cp[i0], cf = cp[i0 + 2];
+                const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
+                const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
+                kmin = min(kmin, min(ke, kf));
+                hmc |= ballot((int)(uint32_t)ce == cell) | ballot((int)(uint32_t)cf == cell);
+            }
+            {
+                const auto r = __builtin_amdgcn_permlane16_swap(kmin, kmin, false, false);
+                kmin = r[0] < r[1] ? r[0] : r[1];
+            }
+            const uint32_t h16 = (uint32_t)(((hmc >> hbase) | (hmc >> (hbase + 16))) & 0xffffull);
+            Mcan = ((h16 >> ri) & 1u) ? ~0u : 0u;
+            const int js = (int)(kmin & 1023u);
+            const int sl = (hbase + (js & 31)) << 2;
+            int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);
+#pragma unroll
+            for (int c = 1; c < NC; c++) {
+                const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
+                bc = (js >> 5) == c ? v : bc;
+            }
+            const bool found = act && kmin != 0xffffffffu;
+            Midle = lmask(found && (kmin >> 21) <= 3u);
+            best_cell = found ? bc : -1;
+        }
+        float cs[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            cs[k] = p.shaping[k];
+            pin(cs[k]);
+        }
+        const int ptg = (int)(g_td & 0xffffu), pdl = (int)(g_td >> 16);
+        const uint32_t Mtg = lmask(cell == ptg);
+        const uint32_t Mpick = Mpc0 & ~Mc0;
+        const uint32_t Mdeliv = ~Mpc0 & Mc0 & Mpres & Mtg;
+        const float t1v = fmask(Mpick, cs[SH_PICK]) + fmask(Mdeliv, fpick(lmask(t1 <= pdl), cs[SH_ONTIME], cs[SH_LATE]));
+        const uint32_t Mwpick = Mop1 & (~Mpc0 | (Mc0 & ~Mcan));
+        const uint32_t Mwdrop = Mop2 & (Mpc0 | (~Mc0 & Mpres & ~Mtg));
+        const float t2v = fmask(Mwpick, cs[SH_WPICK]) + fmask(Mwdrop, cs[SH_WDROP]);
+        const float t3v = fmask(~MS & ~Mmov, cs[SH_STUCK]);
+        const int tgt = ipick(~Mpc0 & Mpres, ptg, best_cell);
+        const int db = manhattan_sad(pcell, tgt), da = manhattan_sad(cell, tgt);
+        const uint32_t Mt = lmask(tgt >= 0) & Mmov;
+        const float t4v = fmask(Mt & lmask(da < db), cs[SH_CLOSER]) + fmask(Mt & lmask(da > db), cs[SH_AWAY]);
+        const float t5v = fmask(~Mmov & MS & Mpc0 & Midle, cs[SH_IDLE]);
+        float s = t1v;
+        s = s + t2v;
+        s = s + t3v;
+        s = s + t4v;
+        s = s + t5v;
+        s_lane = fmask(Mact, s);
+    }
+    // numpy's pairwise float32 sum of the A (8..16) agents, in-row: lanes A..15 hold +0.0f, so every
+    // A in 8..16 takes numpy's n >= 8 form r_j = x_j + x_{j+8}, ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+    float ssum;
+    {
+        const float r8 = s_lane + dppf<0x128>(s_lane);   // row_ror:8: lane j < 8 gets x_j + x_{j+8}
+        const float s2 = r8 + dppf<0xB1>(r8);
+        const float c4 = s2 + dppf<0x4E>(s2);
+        const float d = c4 + dppf<0x124>(c4);           // lane 0: c[0] + c[12] (c[12] == c[4])
+        ssum = 0.0f + row_bcastf<0>(d);
+    }
+    const float shaped = (float)rr + ssum;
+
+    // ---- tracker update with the new state (MAPPO/trainer.py:95-130); halves that reset below
+    // update with the reset state instead ----
+    const bool do_rst = done && auto_reset;
+    const uint64_t rst = ballot(do_rst);
+    if (STALE && (ballot(picked) | dmask | spawned)) {
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const bool ins = !do_rst && (pk_st(pk[c]) == t1) && !(ps[c] & PS_PRESENT);
+            ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
+            td[c] = ins ? pk[c] : td[c];
+            dirty[c] = dirty[c] || ins;
+            const uint32_t m_p = lmask((ps[c] & PS_PRESENT) != 0u && !do_rst);
+            const uint32_t m_c = lmask(((fw >> (8 * c)) & F_CARRY) != 0u);
+            const uint32_t m_t = lmask((ps[c] & PS_TRANSIT) != 0u);
+            ps[c] = (ps[c] | (PS_TRANSIT & m_c & m_p)) & (PS_STATUS | ~(m_p & ~m_c & m_t));
+        }
+    }
+
+    // ---- reset on done (MAPPO/trainer.py:230-235): one half at a time, by the whole wave ----
+    int t_out = do_rst ? 0 : t1;
+    double total_out = do_rst ? 0.0 : total;
+    if (rst) {
+        wave_sync();   // the flag bytes, gather records and candidates are consumed (the reset scratch overlays them)
+        for (uint64_t m = rst & 0x0000000100000001ull; m; m &= m - 1) {
+            const int hb = ffs64(m);   // 32 * the resetting half
+            const int er = e0 + (hb >> 5);
+            ResetLds L = reset_carve(slice, P);
+            const int mr = rdl(mi, hb);
+            const MapDesc md = p.maps[mr];
+            const int nc = do_reset(p, er, md, L, false);   // robot a's cell on lane a
+            const int ncr = __builtin_amdgcn_ds_bpermute(ri << 2, nc);
+            const bool mine = hbase == hb;
+            if (mine && act) {
+                cell = ncr;
+                carry = 0;
+                vmask = p.movevalid_cell[(uint32_t)(mvoff + ncr)];
+            }
+            if (STALE) {
+                // every present entry of the half becomes a survivor ranked by its current key
+                uint32_t rk[NC];
+#pragma unroll
+                for (int c = 0; c < NC; c++) rk[c] = 0;
+#pragma unroll
+                for (int c2 = 0; c2 < NC; c2++) {
+                    uint64_t pm = ballot(c2 * HALF + hl < P && (ps[c2] & PS_PRESENT)) & (0xffffffffull << hb);
+                    while (pm) {
+                        const uint32_t ki = (uint32_t)rdl((int)tq[c2], ffs64(pm));
+                        pm &= pm - 1;
+#pragma unroll
+                        for (int c = 0; c < NC; c++) rk[c] += ki < tq[c] ? 1u : 0u;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < NC; c++) {
+                    if (mine) {
+                        if (c * HALF + hl < P && (ps[c] & PS_PRESENT)) {
+                            tq[c] = rk[c];
+                            ps[c] = (ps[c] & PS_FLAGS) | PS_SURVIVOR | (rk[c] << PS_RANK_SHIFT);
+                        } else {
+                            ps[c] &= PS_STATUS;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const int j = c * HALF + hl;
+                if (mine) {
+                    pk[c] = j < P ? L.pk[j] : ~0ull;
+                    ps[c] = j < P ? ((uint32_t)L.pst[j] | (STALE ? (ps[c] & ~PS_STATUS) : 0u)) : (uint32_t)ST_DELIVERED;
+                    if (STALE) {   // the update with the reset state: inserts at t = 0, nothing carried
+                        const bool ins = (j < P) & (pk_st(pk[c]) == 0) & !(ps[c] & PS_PRESENT);
+                        ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
+                        td[c] = ins ? pk[c] : td[c];
+                        dirty[c] = dirty[c] || ins;
+                        const uint32_t upd = (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
+                        ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
+                    }
+                }
+            }
+            wave_sync();   // L is read by every lane before the next half's reset rewrites it
+        }
+    }
+    vmask = (((moved >> lane) & 1ull) && !do_rst) ? pvm : vmask;
+    asm volatile("" : "+v"(vmask));
+
+    // ---- outputs and write-back (pointers fetched in one late scalar batch) ----
+    GLOBAL double* rop = (GLOBAL double*)kap->r_out;
+    GLOBAL float* shp = (GLOBAL float*)kap->sh_out;
+    GLOBAL uint8_t* dnp = (GLOBAL uint8_t*)kap->done_out;
+    GLOBAL uint32_t* robw = (GLOBAL uint32_t*)kap->p.rob;
+    GLOBAL uint16_t* pstw = (GLOBAL uint16_t*)kap->p.pstate;
+    GLOBAL uint64_t* trkw = (GLOBAL uint64_t*)kap->p.trk;
+    GLOBAL uint64_t* pkgw = (GLOBAL uint64_t*)kap->p.pkg;
+    GLOBAL u32x4* esw = (GLOBAL u32x4*)kap->p.es;
+    const uint32_t er = (uint32_t)h & 1u;
+    if (live && hl == 0) {
+        if (rop) (rop + e0)[er] = rr;
+        if (shp) (shp + e0)[er] = shaped;
+        if (dnp) (dnp + e0)[er] = done ? 1 : 0;
+        (esw + e0)[er] = u32x4{(uint32_t)t_out, rfl, (uint32_t)__double2loint(total_out),
+                               (uint32_t)__double2hiint(total_out)};
+    }
+    if (live && hl == 0 && done) {
+        ((GLOBAL double*)p.ep_total + e0)[er] = total;
+        ((GLOBAL int32_t*)p.ep_len + e0)[er] = t1;
+    }
+    if (act && row0) (robw + (size_t)e0 * A)[roff] = rob_pack(cell, carry, vmask);
+    const bool rhalf = (rst >> lane) & 1ull;   // this half reset: its package table is new
+    const size_t eb = (size_t)e0 * P;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const int j = c * HALF + hl;
+        const uint32_t o = (uint32_t)(h * P + j) & 0xffu;
+        if (pv[c] && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
+        if (rhalf && j < P) (pkgw + eb)[o] = pk[c];
+        if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
+    }
+}

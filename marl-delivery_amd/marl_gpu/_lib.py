@@ -35,6 +35,7 @@ MDL_OBS_BUILDER_GENERIC = 1
 MDL_STEP_LAYOUT_AUTO = 0
 MDL_STEP_LAYOUT_WAVE = 1
 MDL_STEP_LAYOUT_ROWS = 2
+MDL_STEP_LAYOUT_HALVES = 3
 
 
 class MdlConfig(C.Structure):

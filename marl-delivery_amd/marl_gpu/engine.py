@@ -33,7 +33,9 @@ TRACKER_MODES = {"fresh": _lib.MDL_TRACKER_FRESH, "mappo": _lib.MDL_TRACKER_MAPP
                  "mappo_stale": _lib.MDL_TRACKER_MAPPO_STALE}
 ACTION_FORMATS = {"int": _lib.MDL_ACTION_TRAINER_INT, "codes": _lib.MDL_ACTION_CODES}
 OBS_BUILDERS = {"auto": _lib.MDL_OBS_BUILDER_AUTO, "generic": _lib.MDL_OBS_BUILDER_GENERIC}
-STEP_LAYOUTS = {"auto": _lib.MDL_STEP_LAYOUT_AUTO, "wave": _lib.MDL_STEP_LAYOUT_WAVE, "rows": _lib.MDL_STEP_LAYOUT_ROWS}
+STEP_LAYOUTS = {"auto": _lib.MDL_STEP_LAYOUT_AUTO, "wave": _lib.MDL_STEP_LAYOUT_WAVE, "rows": _lib.MDL_STEP_LAYOUT_ROWS,
+                "halves": _lib.MDL_STEP_LAYOUT_HALVES}
+_LAYOUT_NAMES = {_lib.MDL_STEP_LAYOUT_WAVE: "wave", _lib.MDL_STEP_LAYOUT_ROWS: "rows", _lib.MDL_STEP_LAYOUT_HALVES: "halves"}
 STATUS_NAMES = ("None", "waiting", "in_transit", "delivered")
 
 
@@ -60,9 +62,9 @@ class BatchedEnv:
     obs_builder:   "auto" (the small builder where it applies, A <= 8 and P <= 64) or
                "generic" (always the general builder): the same observations either way.
     step_layout:   "auto" (four envs per wavefront for full-batch steps of >= 7,168 envs where A <= 8
-               and P <= 64),
-               "wave" (one env per wavefront) or "rows" (four per wavefront; an error where it does
-               not apply): the same results either way (MdlConfig.step_layout).
+               and P <= 64; two where A == 16, P <= 128 and that is faster), "wave" (one env per
+               wavefront), "rows" (four per wavefront) or "halves" (two per wavefront; both an error
+               where they do not apply): the same results either way (MdlConfig.step_layout).
     After construction every env holds the constructor's layout draw; call
     ``reset()`` for the first episode, as the reference trainers do.
     """
@@ -340,13 +342,13 @@ class BatchedEnv:
         return r, sh, d
 
     def step_layout(self, n: int | None = None) -> str:
-        """The layout ``step`` launches ("wave": one env per wavefront, "rows": four) for the full
+        """The layout ``step`` launches ("wave": one env per wavefront, "rows": four, "halves": two) for the full
         batch (n None) or an ``env_ids`` subset of n envs -- asked of the engine (mdl_step_layout),
         which takes the same decision inside mdl_step."""
         lay = C.c_int32()
         check(lib().mdl_step_layout(self._h, self.E if n is None else int(n), 0 if n is None else 1,
                                     C.byref(lay)), "mdl_step_layout")
-        return {_lib.MDL_STEP_LAYOUT_WAVE: "wave", _lib.MDL_STEP_LAYOUT_ROWS: "rows"}[lay.value]
+        return _LAYOUT_NAMES[lay.value]
 
     def step_kernel_name(self, layout: str | None = None, with_obs: bool = False) -> str:
         """The kernel symbol (as rocprof names it) ``step`` launches in ``layout`` (default: the
@@ -361,7 +363,7 @@ class BatchedEnv:
         """The layout of the last ``step`` launch (None before the first), as the engine recorded it."""
         lay = C.c_int32()
         check(lib().mdl_last_step_layout(self._h, C.byref(lay)), "mdl_last_step_layout")
-        return {0: None, _lib.MDL_STEP_LAYOUT_WAVE: "wave", _lib.MDL_STEP_LAYOUT_ROWS: "rows"}[lay.value]
+        return None if lay.value == 0 else _LAYOUT_NAMES[lay.value]
 
     def step_floor(self, n: int | None = None):
         """Measurement aid: one launch of an empty kernel in ``step``'s launch shape over n envs

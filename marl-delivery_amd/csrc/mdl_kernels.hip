@@ -340,6 +340,8 @@ struct StepKarg {
     StepArgs args;
 };
 constexpr uint32_t NW_IDS = 1u << 29, NW_MAP = 1u << 30;
+// k_step_halves: every map of the engine fits 64 x 64 (the pick-ups' 4096-bit cell maps)
+constexpr uint32_t NW_SMALLMAP = 1u << 31;
 // ap = A (7 bits) | P << 7 (11 bits) | the launch's block count << AP_NB_SHIFT (0 when it does not
 // fit: launch-order slots)
 constexpr int AP_NB_SHIFT = 18;
@@ -1833,7 +1835,9 @@ hipError_t launch_step_halves(const DevParams& p, const uint8_t* actions, int fm
     const int waves = (n + 1) / 2;
     const dim3 grid(blocks_for(waves, wpb)), block(64 * wpb);
     const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
-    const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
+    bool small = true;
+    for (int k = 0; k < p.n_maps; k++) small = small && p.maps[k].H <= 64 && p.maps[k].W <= 64;
+    const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u) | (small ? NW_SMALLMAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a
     if (p.stale) hipLaunchKernelGGL((k_step_halves<true>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
     else hipLaunchKernelGGL((k_step_halves<false>), grid, block, lds * wpb, s, MDL_STEP_ARGS);

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     for (int c = 0; c < NC; c++) {
         const uint32_t f = ps0[c];
         const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
-        wv[c] = waiting && pk_st(td[c]) <= t0;
+        wv[c] = !(MDL_ABLATE & 64) && waiting && pk_st(td[c]) <= t0;
         stc[c] = pk_start(td[c]);
         wvm[c] = ballot(wv[c]);
         anyw |= wvm[c];
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     const int dtab = __builtin_amdgcn_sbfe((int)(uint32_t)(DTAB >> (10 * mv)), 0, 10);
     const int vok = __builtin_amdgcn_sbfe((int)vmask, mv, 1);
     const int prop = cell + (int)(lmask(act) & (uint32_t)(dtab & vok));
-    const bool mover = act && prop != cell;
+    const bool mover = !(MDL_ABLATE & 4) && act && prop != cell;
     const uint64_t movers = ballot(mover);
     const uint32_t pvm = (uint32_t)(p.movevalid_cell + mvoff)[(uint32_t)prop];
     uint64_t moved = 0;
@@ -207,17 +207,25 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         // one word per robot: its proposal if it moves (0xffff otherwise: a non-mover blocks nobody) |
         // its cell << 16 (0xfffe where there is no robot)
         const uint32_t wd = (mover ? (uint32_t)prop : 0xffffu) | ((act ? (uint32_t)cell : 0xfffeu) << 16);
-        uint32_t hit = 0;
-        int occ = -1;
-#define MDL_HMOV(J)                                                      \
-    {                                                                    \
-        const uint32_t wj = (uint32_t)row_bcast<J>((int)wd);             \
-        hit |= (wj & 0xffffu) == (uint32_t)prop ? (1u << J) : 0u;        \
-        occ = (wj >> 16) == (uint32_t)prop ? J : occ;                    \
-    }
-        MDL_HMOV(0) MDL_HMOV(1) MDL_HMOV(2) MDL_HMOV(3) MDL_HMOV(4) MDL_HMOV(5) MDL_HMOV(6) MDL_HMOV(7)
-        MDL_HMOV(8) MDL_HMOV(9) MDL_HMOV(10) MDL_HMOV(11) MDL_HMOV(12) MDL_HMOV(13) MDL_HMOV(14) MDL_HMOV(15)
-#undef MDL_HMOV
+        // Each row tests its robot against half of the partners -- row 0 robots 0-7, row 1 robots
+        // 8-15, fetched from row 0's copies -- and one swap joins the rows' answers.
+        const int g8 = (lane & 16) >> 1;
+        uint32_t hk = 0;
+        int ok = -1;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t wj = (uint32_t)__builtin_amdgcn_ds_bpermute((hbase + g8 + k) << 2, (int)wd);
+            hk |= (wj & 0xffffu) == (uint32_t)prop ? (1u << k) : 0u;
+            ok = (wj >> 16) == (uint32_t)prop ? k : ok;   // robots stand on distinct cells: one match at most
+        }
+        uint32_t hit = hk << g8;
+        int occ = ok < 0 ? -1 : ok + g8;
+        {
+            const auto rh = __builtin_amdgcn_permlane16_swap(hit, hit, false, false);
+            hit = rh[0] | rh[1];
+            const auto ro = __builtin_amdgcn_permlane16_swap((uint32_t)occ, (uint32_t)occ, false, false);
+            occ = max((int)ro[0], (int)ro[1]);
+        }
         // a lower-index mover into the same cell (hit holds movers only)
         const bool blocked = (hit & ((1u << ri) - 1u)) != 0u;
         const uint32_t Mbase = lmask(mover && !blocked), Mfree = lmask(occ < 0);
@@ -238,13 +246,44 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     // Pick-ups: each picking robot takes the lowest-index waiting package at its cell (robots sit on
     // distinct cells, so the reference's robot order changes nothing).  Per robot index J, one
     // minimum over the half's package slots answers robot J of both envs.
-    const bool picker = act && op == 1 && carry == 0;
+    const bool picker = !(MDL_ABLATE & 8) && act && op == 1 && carry == 0;
     const uint64_t pickers = ballot(picker);
     int cnew = carry;
     if (pickers) {
         int sw[NC];
 #pragma unroll
         for (int c = 0; c < NC; c++) sw[c] = (ps[c] & PS_STATUS) == ST_WAITING ? pk_start(pk[c]) : -2;
+        if (nw & NW_SMALLMAP) {
+            // Every map within 64 x 64: each half's pickers mark their cells in a 4096-bit map in LDS
+            // (over the gather records, consumed before the movement); a waiting package tests one
+            // bit, and the few packages under a picker are assigned in index order by the scalar
+            // unit -- the first one at a picker's cell is its lowest-index package.
+            uint32_t* pb = (uint32_t*)slice;
+            auto bit_of = [](int cl) { return ((cl & 63) << 6) | ((cl >> 8) & 63); };
+            wave_sync();
+            reinterpret_cast<u32x4*>(pb)[lane] = u32x4{0u, 0u, 0u, 0u};   // both halves' maps: 1 KB
+            wave_sync();
+            if (picker && row0) {
+                const int ix = bit_of(cell);
+                atomicOr(&pb[h * 128 + (ix >> 5)], 1u << (ix & 31));
+            }
+            wave_sync();
+            uint64_t left = pickers & 0x0000ffff0000ffffull;   // row 0's robot copies
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const int ix = bit_of(sw[c]);   // sw < 0: some in-range bit, masked
+                const uint64_t mt = ballot(sw[c] >= 0 && ((pb[h * 128 + (ix >> 5)] >> (ix & 31)) & 1u));
+                for (uint64_t m = mt; m && left; m &= m - 1) {
+                    const int j = ffs64(m);
+                    const uint64_t who = ballot(cell == rdl(sw[c], j)) & left & (0xffffull << (j & 32));
+                    if (who) {
+                        const int i = ffs64(who);
+                        left &= ~(1ull << i);
+                        cnew = (lane & ~16) == i ? c * HALF + (j & 31) + 1 : cnew;
+                    }
+                }
+            }
+        } else
         for (uint32_t u = rows_union(pickers); u; u &= u - 1) {
             const int J = __ffs((int)u) - 1;
             const int ci = __builtin_amdgcn_ds_bpermute((rbase + J) << 2, cell);   // robot J's cell, row-local
@@ -328,7 +367,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         const uint32_t Mop1 = lmask(op == 1), Mop2 = lmask(op == 2);
         uint32_t Midle = 0, Mcan = 0;
         int best_cell = -1;
-        if (anyw) {
+        if (anyw && !(MDL_ABLATE & 32)) {
             // The two rows of a half scan alternate candidates for the same agent (two per step, two
             // LDS reads in flight): nearest key from the pre-step cell, and "a waiting package starts
             // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.
@@ -403,7 +442,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     // update with the reset state instead ----
     const bool do_rst = done && auto_reset;
     const uint64_t rst = ballot(do_rst);
-    if (STALE && (ballot(picked) | dmask | spawned)) {
+    if (STALE && !(MDL_ABLATE & 2) && (ballot(picked) | dmask | spawned)) {
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             const bool ins = !do_rst && (pk_st(pk[c]) == t1) && !(ps[c] & PS_PRESENT);

@@ -9,7 +9,7 @@ for rep in $(seq 1 ${REPS:-3}); do
   for V in ${VARIANTS:-main}; do
     if [ "$V" = main ]; then L=$R/marl-delivery_amd/marl_gpu/libmdl.so; else L=$R/marl-delivery_amd/build/ab/libmdl_$V.so; fi
     for C in ${CONFIGS:-5}; do
-      MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 200 python3 $R/bench.py --config $C --steps ${STEPS:-300} --warmup 30 \
+      MDL_PROFILING=1 MDL_LIB_PATH=$L timeout -k 10 200 python3 $R/bench.py --config $C ${BENCH_EXTRA:-} --steps ${STEPS:-300} --warmup 30 \
           --cpu-seconds 0 --fused-k 0 --no-floor --graph-only > $O/${V}_${C}_$rep.json 2> $O/${V}_${C}_$rep.err || exit $?
       python3 -c "
 import json

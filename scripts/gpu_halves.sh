@@ -36,3 +36,4 @@ if [ -z "${SKIP_SQ:-}" ]; then
     rc=$?; echo "sq_$L rc=$rc"; [ $rc -ne 0 ] && { tail -20 $O/sq_$L.log; exit $rc; }
   done
 fi
+exit 0

@@ -80,9 +80,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
     uint64_t pk[NC], td[NC];
     uint32_t ps[NC], ps_in[NC], tq[NC];
-    uint32_t dirty[NC];   // 0 / ~0 words in VGPRs (as bools they were SGPR lane masks live across the step)
-    bool pv[NC];
-    uint32_t pvw[NC];
+    bool dirty[NC], pv[NC];
     GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
     GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
     GLOBAL const uint64_t* trke = trkp + (size_t)e0 * P;
@@ -90,12 +88,11 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     for (int c = 0; c < NC; c++) {
         const int j = c * HALF + hl;
         pv[c] = live && j < P;
-        pvw[c] = lmask(pv[c]);
         const uint32_t o = (pv[c] ? (uint32_t)(h * P + j) : 0u) & 0xffu;   // h * P + j < 256
         pk[c] = pkge[o];
         ps[c] = pste[o];
         td[c] = STALE ? trke[o] : 0ull;
-        dirty[c] = 0u;
+        dirty[c] = false;
     }
     const uint32_t erow = (uint32_t)(live ? h : 0) & 1u;
     const uint32_t t_ld = ((GLOBAL const uint32_t*)(esp + e0))[4u * erow];
@@ -451,7 +448,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
             const bool ins = !do_rst && (pk_st(pk[c]) == t1) && !(ps[c] & PS_PRESENT);
             ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
             td[c] = ins ? pk[c] : td[c];
-            dirty[c] |= lmask(ins);
+            dirty[c] = dirty[c] || ins;
             const uint32_t m_p = lmask((ps[c] & PS_PRESENT) != 0u && !do_rst);
             const uint32_t m_c = lmask(((fw >> (8 * c)) & F_CARRY) != 0u);
             const uint32_t m_t = lmask((ps[c] & PS_TRANSIT) != 0u);
@@ -515,7 +512,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
                         const bool ins = (j < P) & (pk_st(pk[c]) == 0) & !(ps[c] & PS_PRESENT);
                         ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
                         td[c] = ins ? pk[c] : td[c];
-                        dirty[c] |= lmask(ins);
+                        dirty[c] = dirty[c] || ins;
                         const uint32_t upd = (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
                         ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
                     }
@@ -555,8 +552,8 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     for (int c = 0; c < NC; c++) {
         const int j = c * HALF + hl;
         const uint32_t o = (uint32_t)(h * P + j) & 0xffu;
-        if (pvw[c] && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
+        if (pv[c] && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
         if (rhalf && j < P) (pkgw + eb)[o] = pk[c];
-        if (STALE && (pvw[c] & dirty[c])) (trkw + eb)[o] = td[c];
+        if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
     }
 }

@@ -131,22 +131,20 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
     uint64_t pk[NC], td[NC];
     uint32_t ps[NC], ps_in[NC], tq[NC];
-    uint32_t dirty[NC];   // 0 / ~0 words in VGPRs (as bools they were SGPR lane masks live across the step)
+    bool dirty[NC];
     GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
     GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
     GLOBAL const uint64_t* trke = trkp + (size_t)e0 * P;
     bool pv[NC];   // package slot c * 16 + rl of this row exists
-    uint32_t pvw[NC];   // the same as a 0 / ~0 word (VGPR) for the stores at the end
 #pragma unroll
     for (int c = 0; c < NC; c++) {
         const int j = c * ROW + rl;
         pv[c] = live && j < P;
-        pvw[c] = lmask(pv[c]);
         const uint32_t o = (pv[c] ? (uint32_t)(r * P + j) : 0u) & 0x1ffu;
         pk[c] = pkge[o];
         ps[c] = pste[o];
         td[c] = STALE ? trke[o] : 0ull;
-        dirty[c] = 0u;
+        dirty[c] = false;
     }
     // the env record's clock and total (its reward-term word is only written): two loads, so no
     // register of an unused component is recycled under a load still in flight (a forced wait)
@@ -472,7 +470,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
             const bool ins = !do_rst && (pk_st(pk[c]) == t1) && !(ps[c] & PS_PRESENT);
             ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
             td[c] = ins ? pk[c] : td[c];
-            dirty[c] |= lmask(ins);
+            dirty[c] = dirty[c] || ins;
             // present entries: carried -> in transit; in transit and not carried -> deleted (status only)
             const uint32_t m_p = lmask((ps[c] & PS_PRESENT) != 0u && !do_rst);
             const uint32_t m_c = lmask(((uint32_t)(fw >> (8 * c)) & F_CARRY) != 0u);
@@ -537,7 +535,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
                         const bool ins = (j < P) & (pk_st(pk[c]) == 0) & !(ps[c] & PS_PRESENT);
                         ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
                         td[c] = ins ? pk[c] : td[c];
-                        dirty[c] |= lmask(ins);
+                        dirty[c] = dirty[c] || ins;
                         const uint32_t upd = (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
                         ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
                     }
@@ -582,8 +580,8 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         // time 0xffff equals t1 once a done env steps on without reset to t = 65535, which "spawns"
         // it (and inserts it into the stale tracker); its masked offset then names the next env's
         // slot, or lies past the allocation for the last env.  (k_step guards its stores with j < P.)
-        if (pvw[c] && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
+        if (pv[c] && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
         if (rrow && j < P) (pkgw + eb)[o] = pk[c];
-        if (STALE && (pvw[c] & dirty[c])) (trkw + eb)[o] = td[c];
+        if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
     }
 }

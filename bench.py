@@ -547,15 +547,17 @@ def main(argv=None):
         per_env = STEP_BYTES_PER_ENV(A, P) + (obs_bytes_env if obs_cfg else 0)
         per_launch_bytes = per_env * E
         achieved = per_launch_bytes / (kdur_us * 1e-6) / 1e9
+        # the kernel the engine launched (its own record and symbol: no Python mirror of its rules)
+        kname = env.step_kernel_name(layout, with_obs=obs_cfg) + (" (mixed maps)" if len(grids) > 1 else "")
         traffic, traffic_rec = None, None
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
                 want = {"envs": E, "agents": A, "packages": P, "maps": args.maps}
                 for rec in tj.get("records", []):
-                    rows_rec = "k_step_rows" in rec.get("kernel", "")
+                    # the PMC pass of the kernel timed here: same workload, same kernel (name prefix)
                     if rec.get("config") == want and bool(rec.get("obs")) == obs_cfg and \
-                            (obs_cfg or rows_rec == (layout == "rows")):   # the PMC pass of the kernel timed here
+                            kname.startswith(rec.get("kernel", "?")):
                         traffic, traffic_rec = rec.get("hbm_bytes_per_launch"), rec
             except (OSError, ValueError):
                 traffic = None
@@ -568,8 +570,6 @@ def main(argv=None):
             cpu = cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, nt, Ec, args.maps[m0], host, obs_cfg)
             cpu1 = cpu if nt == 1 else cpu_baseline(args, grids[m0], seeds[b0], args.cpu_seconds, 1, Ec,
                                                      args.maps[m0], host, obs_cfg)
-        # the kernel the engine launched (its own record and symbol: no Python mirror of its rules)
-        kname = env.step_kernel_name(layout, with_obs=obs_cfg) + (" (mixed maps)" if len(grids) > 1 else "")
         ms_step = wall / K * 1e3
         floor = None
         if wall_floor is not None:

@@ -43,6 +43,21 @@ def test_library_has_gfx950_code_object():
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob or b"amdgcn-amd-amdhsa--gfx950" in blob
 
 
+def test_header_constants_match_python_binding():
+    """Every integer #define MDL_* of include/mdl_engine.h that the ctypes binding names (tracker modes,
+    action formats, builders, step layouts incl. HALVES, limits, reward-term bits) has the same value."""
+    from marl_gpu import _lib
+    txt = open(os.path.join(REPO, "include", "mdl_engine.h")).read()
+    defs = {m.group(1): int(m.group(2)) for m in re.finditer(r"^#define (MDL_[A-Z0-9_]+)\s+(\d+)\b", txt, re.M)}
+    named = [k for k in defs if hasattr(_lib, k)]
+    assert {"MDL_STEP_LAYOUT_AUTO", "MDL_STEP_LAYOUT_WAVE", "MDL_STEP_LAYOUT_ROWS", "MDL_STEP_LAYOUT_HALVES",
+            "MDL_TRACKER_MAPPO_STALE", "MDL_ACTION_CODES", "MDL_OBS_BUILDER_GENERIC"} <= set(named)
+    for k in named:
+        assert getattr(_lib, k) == defs[k], k
+    from marl_gpu import engine
+    assert set(engine.STEP_LAYOUTS.values()) == {defs[k] for k in defs if k.startswith("MDL_STEP_LAYOUT_")}
+
+
 def test_config_struct_layout_matches_c(tmp_path):
     from marl_gpu import _lib
     src = tmp_path / "probe.c"

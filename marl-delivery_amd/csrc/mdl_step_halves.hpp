@@ -191,27 +191,6 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     wave_sync();
     const u32x4 g = grec[((pj >> 5) & (NC - 1)) * 64 + hbase + (pj & 31)];
     const uint32_t g_pf = g.x, g_pk = g.y, g_td = g.z;
-    // Every map within 64 x 64: two 4096-bit cell maps per half in LDS over the gather records (read
-    // just above): the pickers' cells (pick-ups below) and the start cells of the shaped reward's
-    // candidates (its "a waiting package starts at my new cell" test: one bit per agent instead of a
-    // compare and a ballot per candidate in the nearest-package scan).
-    const bool smallmap = (nw & NW_SMALLMAP) != 0;
-    uint32_t* pbits = (uint32_t*)slice;         // [2 halves][128 words] picker cells
-    uint32_t* cbits = (uint32_t*)slice + 256;   // [2 halves][128 words] candidate start cells
-    auto bit_of = [](int cl) { return ((cl & 63) << 6) | ((cl >> 8) & 63); };
-    if (smallmap) {
-        wave_sync();
-        reinterpret_cast<u32x4*>(slice)[lane] = u32x4{0u, 0u, 0u, 0u};
-        reinterpret_cast<u32x4*>(slice)[64 + lane] = u32x4{0u, 0u, 0u, 0u};
-        wave_sync();
-        if (anyw) {
-#pragma unroll
-            for (int c = 0; c < NC; c++) {
-                const int ix = bit_of(stc[c]);
-                if (wv[c]) atomicOr(&cbits[h * 128 + (ix >> 5)], 1u << (ix & 31));
-            }
-        }
-    }
 
     // ---- movement (env.py:188-257), row-local: every row holds its half's 16 robots ----
     const int pcell = cell, pcarry = carry;
@@ -274,11 +253,16 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         int sw[NC];
 #pragma unroll
         for (int c = 0; c < NC; c++) sw[c] = (ps[c] & PS_STATUS) == ST_WAITING ? pk_start(pk[c]) : -2;
-        if (smallmap) {
-            // each half's pickers mark their cells (the cleared map above); a waiting package tests
-            // one bit, and the few packages under a picker are assigned in index order by the scalar
-            // unit -- the first one at a picker's cell is its lowest-index package
-            uint32_t* pb = pbits;
+        if (nw & NW_SMALLMAP) {
+            // Every map within 64 x 64: each half's pickers mark their cells in a 4096-bit map in LDS
+            // (over the gather records, consumed before the movement); a waiting package tests one
+            // bit, and the few packages under a picker are assigned in index order by the scalar
+            // unit -- the first one at a picker's cell is its lowest-index package.
+            uint32_t* pb = (uint32_t*)slice;
+            auto bit_of = [](int cl) { return ((cl & 63) << 6) | ((cl >> 8) & 63); };
+            wave_sync();
+            reinterpret_cast<u32x4*>(pb)[lane] = u32x4{0u, 0u, 0u, 0u};   // both halves' maps: 1 KB
+            wave_sync();
             if (picker && row0) {
                 const int ix = bit_of(cell);
                 atomicOr(&pb[h * 128 + (ix >> 5)], 1u << (ix & 31));
@@ -389,31 +373,20 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
             // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.
             const uint64_t* cp = cand + ((lane >> 4) & 1);
             uint32_t kmin = 0xffffffffu;
-            if (smallmap) {
-                const int ix = bit_of(cell);
-                Mcan = ((cbits[h * 128 + (ix >> 5)] >> (ix & 31)) & 1u) ? ~0u : 0u;
-                for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
-                    const uint64_t ce = cp[i0], cf = cp[i0 + 2];
-                    const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
-                    const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
-                    kmin = min(kmin, min(ke, kf));
-                }
-            } else {
-                uint64_t hmc = 0;
-                for (int i0 = 0; i0 < nwg; i0 += 4) {
-                    const uint64_t ce = cp[i0], cf = cp[i0 + 2];
-                    const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
-                    const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
-                    kmin = min(kmin, min(ke, kf));
-                    hmc |= ballot((int)(uint32_t)ce == cell) | ballot((int)(uint32_t)cf == cell);
-                }
-                const uint32_t h16 = (uint32_t)(((hmc >> hbase) | (hmc >> (hbase + 16))) & 0xffffull);
-                Mcan = ((h16 >> ri) & 1u) ? ~0u : 0u;
+            uint64_t hmc = 0;
+            for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
+                const uint64_t ce = cp[i0], cf = cp[i0 + 2];
+                const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
+                const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
+                kmin = min(kmin, min(ke, kf));
+                hmc |= ballot((int)(uint32_t)ce == cell) | ballot((int)(uint32_t)cf == cell);
             }
             {
                 const auto r = __builtin_amdgcn_permlane16_swap(kmin, kmin, false, false);
                 kmin = r[0] < r[1] ? r[0] : r[1];
             }
+            const uint32_t h16 = (uint32_t)(((hmc >> hbase) | (hmc >> (hbase + 16))) & 0xffffull);
+            Mcan = ((h16 >> ri) & 1u) ? ~0u : 0u;
             const int js = (int)(kmin & 1023u);
             const int sl = (hbase + (js & 31)) << 2;
             int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);

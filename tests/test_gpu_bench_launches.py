@@ -12,7 +12,10 @@ item 1).
   65,536 envs of map1..map5 (contiguous map groups, seeds 42 + global id).  Here that batch runs 45
   steps across an auto-reset with oracle windows at the start, at every map-group boundary
   (13,108, 26,215, 39,322, 52,429) and at the last wave; state, tracker rows and vectors at the end.
-* Both tests assert which kernel the engine launched (``mdl_last_step_layout`` /
+* Config 5: ``bench.py --config 5`` at one GPU times ONE ``k_step_halves<true>`` launch over 131,072
+  envs (64x64, 16 robots, 100 packages); the same batch runs 45 steps across an auto-reset with
+  oracle windows at the start, the middle, an XCD-slot boundary and the last wave.
+* The tests assert which kernel the engine launched (``mdl_last_step_layout`` /
   ``mdl_step_kernel_name``), the record bench.py labels its roofline with.
 """
 import numpy as np
@@ -122,4 +125,46 @@ def test_config4_rows_65536_five_maps_vs_oracle():
             np.testing.assert_array_equal(av[i], want)
             _, gv = O.convert_global_state(grids[m], os_["t"], rb1, rows, T, 100, 100)
             np.testing.assert_array_equal(cv[i], gv)
+    env.close()
+
+
+def test_config5_halves_131072_vs_oracle():
+    """Config 5 at one GPU: ``bench.py --config 5`` times ONE ``k_step_halves<true>`` launch over
+    131,072 envs of the 64x64 map (16 robots, 100 packages; the layout AUTO takes there).  Here that
+    batch runs 45 steps across an auto-reset (T = 30) with oracle windows at the start, around the
+    middle, at an XCD-slot boundary and at the last wave: rewards, shaped rewards and dones every
+    step, state and tracker rows at the end."""
+    import marl_gpu as mg
+    g = grid("synthetic64.txt")
+    E, A, P, T, W = 131072, 16, 100, 30, 6
+    env = mg.BatchedEnv(g, E, A, P, T, seed=42, tracker="mappo", shaping="mappo", max_other_robots=15,
+                        max_packages_obs=20, max_robots_state=16, max_packages_state=100)
+    env.reset()
+    assert env.step_layout() == "halves" and env.step_kernel_name() == "mdl::k_step_halves<true>"
+    starts = [0, 16381, 65533, 98304 - 3, E - W]
+    wins = [(s, O.OracleBatch(W, g, A, P, T, seed_base=42 + s, clear_on_reset=False)) for s in starts]
+    gen = np.random.RandomState(55)
+    dones = 0
+    for k in range(45):
+        ints = gen.randint(0, 15, size=(E, A)).astype(np.uint8)
+        r, sh, d = env.step(torch.from_numpy(ints).cuda())
+        assert env.last_step_layout() == "halves"
+        rh, shh, dh = r.cpu().numpy(), sh.cpu().numpy(), d.cpu().numpy().astype(bool)
+        dones += int(dh.sum())
+        for s, ob in wins:
+            r0, s0, d0 = ob.step(ints[s:s + W], auto_reset=True, consts=O.MAPPO_CONSTS)
+            np.testing.assert_array_equal(rh[s:s + W], r0, err_msg=f"r_env step {k} envs {s}+")
+            np.testing.assert_array_equal(shh[s:s + W], s0, err_msg=f"shaped step {k} envs {s}+")
+            np.testing.assert_array_equal(dh[s:s + W], d0, err_msg=f"done step {k} envs {s}+")
+    assert dones == E
+    st = env.read_state()
+    torch.cuda.synchronize()
+    st = {k: v.cpu().numpy() for k, v in st.items()}
+    for s, ob in wins:
+        for i in range(W):
+            os_ = ob.env(i).state()
+            assert st["t"][s + i] == os_["t"] and st["total_reward"][s + i] == os_["total_reward"]
+            np.testing.assert_array_equal(st["robots"][s + i], os_["robots"])
+            np.testing.assert_array_equal(st["pkgs"][s + i], os_["pkgs"])
+            np.testing.assert_array_equal(env.tracker_rows(st, s + i), ob.tracker(i).rows(), err_msg=f"env {s + i}")
     env.close()

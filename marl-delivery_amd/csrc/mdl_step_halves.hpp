@@ -369,24 +369,33 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         int best_cell = -1;
         if (anyw && !(MDL_ABLATE & 32)) {
             // The two rows of a half scan alternate candidates for the same agent (two per step, two
-            // LDS reads in flight): nearest key from the pre-step cell, and "a waiting package starts
-            // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.
+            // LDS reads in flight) for the nearest key from the pre-step cell; one swap joins the rows.
             const uint64_t* cp = cand + ((lane >> 4) & 1);
             uint32_t kmin = 0xffffffffu;
-            uint64_t hmc = 0;
             for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
                 const uint64_t ce = cp[i0], cf = cp[i0 + 2];
                 const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
                 const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
                 kmin = min(kmin, min(ke, kf));
-                hmc |= ballot((int)(uint32_t)ce == cell) | ballot((int)(uint32_t)cf == cell);
             }
             {
                 const auto r = __builtin_amdgcn_permlane16_swap(kmin, kmin, false, false);
                 kmin = r[0] < r[1] ? r[0] : r[1];
             }
-            const uint32_t h16 = (uint32_t)(((hmc >> hbase) | (hmc >> (hbase + 16))) & 0xffffull);
-            Mcan = ((h16 >> ri) & 1u) ? ~0u : 0u;
+            // "A waiting package starts at my new cell" (the can-pick-up test) matters only for
+            // agents with op 1 that carry nothing before and after the step (Mwpick below): per such
+            // robot index, one compare per package slot of its half and a ballot -- instead of a
+            // compare and a ballot per candidate in the scan above for every agent.
+            const bool need_can = act && op == 1 && pcarry == 0 && carry == 0;
+            for (uint32_t u = rows_union(ballot(need_can)); u; u &= u - 1) {
+                const int J = __ffs((int)u) - 1;
+                const int ca = __builtin_amdgcn_ds_bpermute((rbase + J) << 2, cell);   // robot J's new cell
+                bool hit = false;
+#pragma unroll
+                for (int c = 0; c < NC; c++) hit = hit | (wv[c] && stc[c] == ca);
+                const uint64_t hm = ballot(hit);
+                Mcan = (ri == J && ((hm >> hbase) & 0xffffffffull) != 0ull) ? ~0u : Mcan;
+            }
             const int js = (int)(kmin & 1023u);
             const int sl = (hbase + (js & 31)) << 2;
             int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);

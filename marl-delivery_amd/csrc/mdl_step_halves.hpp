@@ -372,6 +372,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
             // LDS reads in flight) for the nearest key from the pre-step cell; one swap joins the rows.
             const uint64_t* cp = cand + ((lane >> 4) & 1);
             uint32_t kmin = 0xffffffffu;
+#pragma nounroll
             for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
                 const uint64_t ce = cp[i0], cf = cp[i0 + 2];
                 const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);

@@ -97,7 +97,8 @@ def parse(argv=None):
                     help="process-group backend under torchrun (gloo: rehearse N ranks on fewer GPUs)")
     ap.add_argument("--step-layout", default="auto", choices=("auto", "wave", "rows", "halves"),
                     help="mdl_step's env-to-wavefront mapping (MdlConfig.step_layout; same results): auto = four "
-                         "envs per wavefront where A <= 8 and P <= 64")
+                         "envs per wavefront where A <= 8 and P <= 64 (>= 7,168 envs), two where A == 16 and "
+                         "P <= 128 (>= 12,288 envs)")
     ap.add_argument("--host-wait", default="auto", choices=("auto", "spin", "yield", "blocking"),
                     help="how the host waits for the GPU in synchronize (hipSetDeviceFlags schedule mode)")
     ap.add_argument("--no-strong", action="store_true",

@@ -70,8 +70,8 @@ typedef struct {
 /* MdlConfig.step_layout.  ROWS: a full-batch mdl_step (env_ids NULL) runs four envs per wavefront,
  * one per 16-lane row (A <= 8, P <= 64; mdl_create fails otherwise).  HALVES: two envs per
  * wavefront, one per 32-lane half (A == 16, P <= 128).  WAVE: one env per wavefront always.  AUTO:
- * ROWS where it applies and the batch has at least 7,168 envs, HALVES where it applies and is the
- * faster layout (see MdlEngine::HALVES_MIN_ENVS), WAVE otherwise.  Subset steps (env_ids),
+ * ROWS where it applies and the batch has at least 7,168 envs, HALVES where it applies and the
+ * batch has at least 12,288 envs (the measured crossovers on MI355X), WAVE otherwise.  Subset steps (env_ids),
  * mdl_step_fused, mdl_step_obs and the mailbox step always use one wave per env.  Every layout
  * produces the same state and outputs; the explicit layouts exist so tests can compare them on one
  * configuration. */

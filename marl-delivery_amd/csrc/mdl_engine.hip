@@ -132,8 +132,11 @@ struct MdlEngine {
     // config 4's 65,536 28.7 vs 21.1; profiles/r05/rows_ab.txt).
     static constexpr int ROWS_MIN_ENVS = 7168;
     bool rows_for(int n) const { return step_rows && (rows_forced || n >= ROWS_MIN_ENVS); }
-    // Two envs per wavefront (k_step_halves) from HALVES_MIN_ENVS envs on (AUTO).
-    static constexpr int HALVES_MIN_ENVS = 1 << 30;   // not chosen by AUTO until measured
+    // Two envs per wavefront (k_step_halves, A == 16, P <= 128) from HALVES_MIN_ENVS envs on (AUTO):
+    // below it one wave per env is as fast (8,192 envs: 8.56 vs 8.67 us per step), from 16,384 on the
+    // halves layout is faster (13.65 vs 14.08, 65,536: 41.3 vs 45.6, config 5's 131,072: 76.1 vs
+    // 84.1; profiles/r06/ab3/ab.txt).
+    static constexpr int HALVES_MIN_ENVS = 12288;
     bool halves_for(int n) const { return step_halves && (halves_forced || n >= HALVES_MIN_ENVS); }
     // the layout mdl_step launches for a call over n envs (with an id list: always one wave per env)
     int32_t layout_for(int n, bool ids) const {

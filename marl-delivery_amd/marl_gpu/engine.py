@@ -62,7 +62,7 @@ class BatchedEnv:
     obs_builder:   "auto" (the small builder where it applies, A <= 8 and P <= 64) or
                "generic" (always the general builder): the same observations either way.
     step_layout:   "auto" (four envs per wavefront for full-batch steps of >= 7,168 envs where A <= 8
-               and P <= 64; two where A == 16, P <= 128 and that is faster), "wave" (one env per
+               and P <= 64; two for >= 12,288 envs where A == 16 and P <= 128), "wave" (one env per
                wavefront), "rows" (four per wavefront) or "halves" (two per wavefront; both an error
                where they do not apply): the same results either way (MdlConfig.step_layout).
     After construction every env holds the constructor's layout draw; call

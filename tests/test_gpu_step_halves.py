@@ -138,3 +138,26 @@ def test_halves_vs_oracle_config5(tracker):
                 assert s["t"][e] == os_["t"] and s["total_reward"][e] == os_["total_reward"]
                 np.testing.assert_array_equal(env.tracker_rows(s, e), ob.tracker(e).rows(), err_msg=f"tracker env {e}")
     env.close()
+
+
+def test_halves_auto_threshold():
+    """auto: one wave per env below 12,288 envs, two per wave from there on (A == 16, P <= 128) -- the
+    engine's own decision (mdl_step_layout) and what its launches record; same results."""
+    import marl_gpu as mg
+    g = grid("synthetic64.txt")
+    small = mg.BatchedEnv(g, 12287, 16, 100, 20, seed=1)
+    big = mg.BatchedEnv(g, 12288, 16, 100, 20, seed=1)
+    assert small.step_layout() == "wave" and big.step_layout() == "halves"
+    assert mg.BatchedEnv(g, 20000, 16, 129, 20, seed=1).step_layout() == "wave"   # P > 128
+    ref = mg.BatchedEnv(g, 12288, 16, 100, 20, seed=1, step_layout="wave")
+    for e in (big, ref):
+        e.reset()
+    gen = torch.Generator(device="cuda").manual_seed(13)
+    for k in range(25):
+        acts = torch.randint(0, 15, (12288, 16), dtype=torch.uint8, device="cuda", generator=gen)
+        r1, s1, d1 = big.step(acts)
+        assert big.last_step_layout() == "halves"
+        r2, s2, d2 = ref.step(acts)
+        assert torch.equal(r1, r2) and torch.equal(s1.view(torch.int32), s2.view(torch.int32)) and torch.equal(d1, d2)
+    torch.cuda.synchronize()
+    assert np.array_equal(big.save_state(), ref.save_state())

@@ -34,10 +34,11 @@ __device__ __forceinline__ uint32_t half_min_u32(uint32_t m) {
     return r[0] < r[1] ? r[0] : r[1];
 }
 
-// LDS bytes per wave: the carried-package gather records (4 chunks x 64 lanes x 16 B), the flag bytes
-// (64 lanes x 4), the two halves' candidate lists; the reset scratch reuses the slice.
+// LDS bytes per wave: the carried-package gather records (4 chunks x 64 lanes x (8 + 2) B), the flag
+// bytes (64 lanes x 4), the two halves' candidate lists; the reset scratch reuses the slice.
+constexpr size_t HALF_GREC = (size_t)HALF_NC * 64 * 8, HALF_GPS = (size_t)HALF_NC * 64 * 2;
 __host__ __device__ constexpr size_t halves_scratch_bytes() {
-    return (size_t)HALF_NC * 64 * 16 + 64 * (size_t)HALF_NC + 2 * (size_t)HALF_CAND * 8;
+    return HALF_GREC + HALF_GPS + 64 * (size_t)HALF_NC + 2 * (size_t)HALF_CAND * 8;
 }
 
 template <bool STALE>
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         wvm[c] = ballot(wv[c]);
         anyw |= wvm[c];
     }
-    uint64_t* cand = (uint64_t*)(slice + NC * 64 * 16 + 64 * NC) + h * HALF_CAND;   // this lane's half
+    uint64_t* cand = (uint64_t*)(slice + HALF_GREC + HALF_GPS + 64 * NC) + h * HALF_CAND;   // this lane's half
     int nwg = 0;
     if (anyw) {
         const uint64_t hm = h ? 0xffffffff00000000ull : 0x00000000ffffffffull;
@@ -183,14 +184,19 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
 
     // ---- the pre-step carried package of each robot, through LDS; the flag bytes cleared ----
     const int pj = carry - 1;
-    u32x4* grec = (u32x4*)slice;
-    unsigned char* flb = slice + NC * 64 * 16;   // byte (lane, c) <-> package slot c * 32 + (lane & 31) of the half
+    uint64_t* grec = (uint64_t*)slice;                    // env-table | tracker target | deadline << 16
+    uint16_t* gps = (uint16_t*)(slice + HALF_GREC);       // the pre-step state word
+    unsigned char* flb = slice + HALF_GREC + HALF_GPS;    // byte (lane, c) <-> package slot c * 32 + (lane & 31) of the half
 #pragma unroll
-    for (int c = 0; c < NC; c++) grec[c * 64 + lane] = u32x4{ps0[c], tgt_dl(pk[c]), tgt_dl(td[c]), 0u};
+    for (int c = 0; c < NC; c++) {
+        grec[c * 64 + lane] = (uint64_t)tgt_dl(pk[c]) | ((uint64_t)tgt_dl(td[c]) << 32);
+        gps[c * 64 + lane] = (uint16_t)ps0[c];
+    }
     ((uint32_t*)flb)[lane] = 0;
     wave_sync();
-    const u32x4 g = grec[((pj >> 5) & (NC - 1)) * 64 + hbase + (pj & 31)];
-    const uint32_t g_pf = g.x, g_pk = g.y, g_td = g.z;
+    const int gi = ((pj >> 5) & (NC - 1)) * 64 + hbase + (pj & 31);
+    const uint64_t gv = grec[gi];
+    const uint32_t g_pf = gps[gi], g_pk = (uint32_t)gv, g_td = (uint32_t)(gv >> 32);
 
     // ---- movement (env.py:188-257), row-local: every row holds its half's 16 robots ----
     const int pcell = cell, pcarry = carry;
@@ -369,34 +375,24 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         int best_cell = -1;
         if (anyw && !(MDL_ABLATE & 32)) {
             // The two rows of a half scan alternate candidates for the same agent (two per step, two
-            // LDS reads in flight) for the nearest key from the pre-step cell; one swap joins the rows.
+            // LDS reads in flight): nearest key from the pre-step cell, and "a waiting package starts
+            // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.
             const uint64_t* cp = cand + ((lane >> 4) & 1);
             uint32_t kmin = 0xffffffffu;
-#pragma nounroll
+            uint64_t hmc = 0;
             for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
                 const uint64_t ce = cp[i0], cf = cp[i0 + 2];
                 const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
                 const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
                 kmin = min(kmin, min(ke, kf));
+                hmc |= ballot((int)(uint32_t)ce == cell) | ballot((int)(uint32_t)cf == cell);
             }
             {
                 const auto r = __builtin_amdgcn_permlane16_swap(kmin, kmin, false, false);
                 kmin = r[0] < r[1] ? r[0] : r[1];
             }
-            // "A waiting package starts at my new cell" (the can-pick-up test) matters only for
-            // agents with op 1 that carry nothing before and after the step (Mwpick below): per such
-            // robot index, one compare per package slot of its half and a ballot -- instead of a
-            // compare and a ballot per candidate in the scan above for every agent.
-            const bool need_can = act && op == 1 && pcarry == 0 && carry == 0;
-            for (uint32_t u = rows_union(ballot(need_can)); u; u &= u - 1) {
-                const int J = __ffs((int)u) - 1;
-                const int ca = __builtin_amdgcn_ds_bpermute((rbase + J) << 2, cell);   // robot J's new cell
-                bool hit = false;
-#pragma unroll
-                for (int c = 0; c < NC; c++) hit = hit | (wv[c] && stc[c] == ca);
-                const uint64_t hm = ballot(hit);
-                Mcan = (ri == J && ((hm >> hbase) & 0xffffffffull) != 0ull) ? ~0u : Mcan;
-            }
+            const uint32_t h16 = (uint32_t)(((hmc >> hbase) | (hmc >> (hbase + 16))) & 0xffffull);
+            Mcan = ((h16 >> ri) & 1u) ? ~0u : 0u;
             const int js = (int)(kmin & 1023u);
             const int sl = (hbase + (js & 31)) << 2;
             int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);

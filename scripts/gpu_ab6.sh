@@ -8,7 +8,8 @@ R=$(pwd)
 O=$R/gpurun_out/r06/${TAG:-ab}
 mkdir -p $O
 if [ -n "${CAND:-}" ]; then
-  MDL_PROFILING=1 MDL_LIB_PATH=$R/marl-delivery_amd/build/ab/libmdl_$CAND.so timeout -k 10 600 \
+  if [ "$CAND" = main ]; then CL=$R/marl-delivery_amd/marl_gpu/libmdl.so; else CL=$R/marl-delivery_amd/build/ab/libmdl_$CAND.so; fi
+  MDL_PROFILING=1 MDL_LIB_PATH=$CL timeout -k 10 600 \
     python -u -m pytest ${TESTS:-tests/test_gpu_step_halves.py} -x -q -p no:cacheprovider --timeout 300 --timeout-method thread \
     > $O/pytest_$CAND.out 2>&1
   rc=$?; tail -3 $O/pytest_$CAND.out; [ $rc -ne 0 ] && { tail -40 $O/pytest_$CAND.out; exit $rc; }

@@ -24,4 +24,5 @@ run bench_long 300 python bench.py --cpu-seconds 0 --steps 2000 --warmup 200
 run bench_gpus2 300 python bench.py --gpus 2 --backend gloo --steps 40 --warmup 5 --cpu-seconds 2 --gather
 run bench_c3 300 python bench.py --config 3 --steps 200 --warmup 20 --cpu-seconds 4
 run bench_c4 300 python bench.py --config 4 --steps 200 --warmup 20 --cpu-seconds 2 --fused-k 0
-run bench_c5 300 python bench.py --config 5 --steps 200 --warmup 20 --cpu-seconds 0 --fused-k 0
+run bench_c5 300 python bench.py --config 5 --steps 200 --warmup 20 --cpu-seconds 2 --fused-k 0
+exit 0

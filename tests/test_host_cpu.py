@@ -43,6 +43,17 @@ def test_library_has_gfx950_code_object():
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob or b"amdgcn-amd-amdhsa--gfx950" in blob
 
 
+def test_makefile_lists_every_kernel_header():
+    """Every header under csrc/ and include/ is a dependency of the library's objects in the Makefile
+    (a header missing from HDR left a stale kernel in libmdl.so after an edit, round 6)."""
+    mk = open(os.path.join(REPO, "marl-delivery_amd", "Makefile")).read()
+    hdr = re.search(r"^HDR\s*=\s*(.*)$", mk, re.M).group(1).split()
+    for f in sorted(os.listdir(os.path.join(REPO, "marl-delivery_amd", "csrc"))):
+        if f.endswith(".hpp"):
+            assert "csrc/" + f in hdr, f"csrc/{f} missing from the Makefile's HDR"
+    assert "../include/mdl_engine.h" in hdr
+
+
 def test_header_constants_match_python_binding():
     """Every integer #define MDL_* of include/mdl_engine.h that the ctypes binding names (tracker modes,
     action formats, builders, step layouts incl. HALVES, limits, reward-term bits) has the same value."""

@@ -80,7 +80,8 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     const uint32_t rv_ld = (robp + (size_t)e0 * A)[roff_c];
     const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
     uint64_t pk[NC], td[NC];
-    uint32_t ps[NC], ps_in[NC], tq[NC];
+    uint32_t ps[NC];
+    uint32_t ps_in[NC / 2];   // the loaded state words, two 16-bit words per register (compared at the stores)
     bool dirty[NC], pv[NC];
     GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
     GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
@@ -113,7 +114,8 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         pk[c] = pv[c] ? pk[c] : ~0ull;
         ps[c] = pv[c] ? ps[c] : (uint32_t)ST_DELIVERED;
         td[c] = pv[c] ? td[c] : ~0ull;
-        ps_in[c] = ps[c];
+        if (c & 1) ps_in[c >> 1] |= ps[c] << 16;
+        else ps_in[c >> 1] = ps[c];
     }
     const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride;
     const int T = p.T;
@@ -137,19 +139,18 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     uint32_t ps0[NC];
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        const int j = c * HALF + hl;
         ps0[c] = ps[c];
-        if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
-            td[c] = pk[c];
-            tq[c] = STALE ? ORD_EPISODE + (uint32_t)j : (uint32_t)j;
-        } else {
-            tq[c] = ps0[c] >> PS_RANK_SHIFT;
-        }
+        if (!STALE || !(ps0[c] & PS_SURVIVOR)) td[c] = pk[c];
     }
+    // tracker_prev's dict-order key of slot j: a survivor's rank, else ORD_EPISODE + j (stale mode),
+    // recomputed where it is needed (registers are this kernel's occupancy limit)
+    auto order_key = [&](uint32_t f, int j) -> uint32_t {
+        return STALE ? ((f & PS_SURVIVOR) ? (f >> PS_RANK_SHIFT) : ORD_EPISODE + (uint32_t)j) : (uint32_t)j;
+    };
 
     // ---- the shaped reward's candidates (tracker_prev's waiting entries with st <= t): pre-step
-    // state only, packed now into each half's LDS list {start cell, order key << 10 | slot} ----
-    int stc[NC];
+    // state only, packed now into each half's LDS list {start cell, order key << 10 | list index}
+    // (order keys are distinct, so the index only names the winner: its start cell is one LDS read) ----
     uint64_t anyw = 0, wvm[NC];
     bool wv[NC];
 #pragma unroll
@@ -157,7 +158,6 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         const uint32_t f = ps0[c];
         const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
         wv[c] = !(MDL_ABLATE & 64) && waiting && pk_st(td[c]) <= t0;
-        stc[c] = pk_start(td[c]);
         wvm[c] = ballot(wv[c]);
         anyw |= wvm[c];
     }
@@ -170,8 +170,8 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             const int idx = nh + popc64(wvm[c] & lt);
-            const uint32_t klo = (tq[c] << 10) | (uint32_t)(c * HALF + hl);
-            if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo << 32);
+            const uint32_t klo = (order_key(ps0[c], c * HALF + hl) << 10) | (uint32_t)idx;
+            if (wv[c]) cand[idx] = (uint64_t)(uint32_t)pk_start(td[c]) | ((uint64_t)klo << 32);
             n0 += popc64(wvm[c] & 0x00000000ffffffffull);
             n1 += popc64(wvm[c] & 0xffffffff00000000ull);
             nh = h ? n1 : n0;
@@ -379,28 +379,32 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
             // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.
             const uint64_t* cp = cand + ((lane >> 4) & 1);
             uint32_t kmin = 0xffffffffu;
-            uint64_t hmc = 0;
+#pragma nounroll
             for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
                 const uint64_t ce = cp[i0], cf = cp[i0 + 2];
                 const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
                 const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
                 kmin = min(kmin, min(ke, kf));
-                hmc |= ballot((int)(uint32_t)ce == cell) | ballot((int)(uint32_t)cf == cell);
             }
             {
                 const auto r = __builtin_amdgcn_permlane16_swap(kmin, kmin, false, false);
                 kmin = r[0] < r[1] ? r[0] : r[1];
             }
-            const uint32_t h16 = (uint32_t)(((hmc >> hbase) | (hmc >> (hbase + 16))) & 0xffffull);
-            Mcan = ((h16 >> ri) & 1u) ? ~0u : 0u;
-            const int js = (int)(kmin & 1023u);
-            const int sl = (hbase + (js & 31)) << 2;
-            int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);
+            // "A waiting package starts at my new cell" (the can-pick-up test) matters only for agents
+            // with op 1 that carry nothing before and after the step (Mwpick below): per such robot
+            // index, one compare per package slot of its half and a ballot -- not a compare and a
+            // ballot per candidate in the scan for every agent.
+            const bool need_can = act && op == 1 && pcarry == 0 && carry == 0;
+            for (uint32_t u = rows_union(ballot(need_can)); u; u &= u - 1) {
+                const int J = __ffs((int)u) - 1;
+                const int ca = __builtin_amdgcn_ds_bpermute((rbase + J) << 2, cell);   // robot J's new cell
+                bool hit = false;
 #pragma unroll
-            for (int c = 1; c < NC; c++) {
-                const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
-                bc = (js >> 5) == c ? v : bc;
+                for (int c = 0; c < NC; c++) hit = hit | (wv[c] && pk_start(td[c]) == ca);
+                const uint64_t hm = ballot(hit);
+                Mcan = (ri == J && ((hm >> hbase) & 0xffffffffull) != 0ull) ? ~0u : Mcan;
             }
+            const int bc = (int)(uint32_t)cand[kmin & 127u];   // the nearest candidate's start cell
             const bool found = act && kmin != 0xffffffffu;
             Midle = lmask(found && (kmin >> 21) <= 3u);
             best_cell = found ? bc : -1;
@@ -462,30 +466,68 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         }
     }
 
-    // ---- reset on done (MAPPO/trainer.py:230-235): one half at a time, by the whole wave ----
-    int t_out = do_rst ? 0 : t1;
-    double total_out = do_rst ? 0.0 : total;
+    // ---- outputs and write-back of the step (pointers fetched in one late scalar batch).  A half
+    // that resets stores only its outputs and env record here: the reset below writes its rows,
+    // after these stores, so the package registers are dead while it runs (the reset path would
+    // otherwise set the kernel's register count: 85 VGPRs and 28 SGPR spills, against 72 and none) ----
+    const int t_out = do_rst ? 0 : t1;
+    const double total_out = do_rst ? 0.0 : total;
+    vmask = (((moved >> lane) & 1ull) && !do_rst) ? pvm : vmask;
+    asm volatile("" : "+v"(vmask));
+    GLOBAL double* rop = (GLOBAL double*)kap->r_out;
+    GLOBAL float* shp = (GLOBAL float*)kap->sh_out;
+    GLOBAL uint8_t* dnp = (GLOBAL uint8_t*)kap->done_out;
+    GLOBAL uint32_t* robw = (GLOBAL uint32_t*)kap->p.rob;
+    GLOBAL uint16_t* pstw = (GLOBAL uint16_t*)kap->p.pstate;
+    GLOBAL uint64_t* trkw = (GLOBAL uint64_t*)kap->p.trk;
+    GLOBAL u32x4* esw = (GLOBAL u32x4*)kap->p.es;
+    const uint32_t er = (uint32_t)h & 1u;
+    if (live && hl == 0) {
+        if (rop) (rop + e0)[er] = rr;
+        if (shp) (shp + e0)[er] = shaped;
+        if (dnp) (dnp + e0)[er] = done ? 1 : 0;
+        (esw + e0)[er] = u32x4{(uint32_t)t_out, rfl, (uint32_t)__double2loint(total_out),
+                               (uint32_t)__double2hiint(total_out)};
+    }
+    if (live && hl == 0 && done) {
+        ((GLOBAL double*)p.ep_total + e0)[er] = total;
+        ((GLOBAL int32_t*)p.ep_len + e0)[er] = t1;
+    }
+    if (act && row0 && !do_rst) (robw + (size_t)e0 * A)[roff] = rob_pack(cell, carry, vmask);
+    const size_t eb = (size_t)e0 * P;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const int j = c * HALF + hl;
+        const uint32_t o = (uint32_t)(h * P + j) & 0xffu;
+        // (dirty marks inserts of this step, which a resetting half does not make)
+        if (pv[c] && !do_rst && ps[c] != ((ps_in[c >> 1] >> (16 * (c & 1))) & 0xffffu)) (pstw + eb)[o] = (uint16_t)ps[c];
+        if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
+    }
+
+    // ---- reset on done (MAPPO/trainer.py:230-235): one half at a time, by the whole wave; it writes
+    // the half's robots, package table and state words (and the tracker's t = 0 inserts) ----
     if (rst) {
+        GLOBAL uint64_t* pkgw = (GLOBAL uint64_t*)kap->p.pkg;
         wave_sync();   // the flag bytes, gather records and candidates are consumed (the reset scratch overlays them)
         for (uint64_t m = rst & 0x0000000100000001ull; m; m &= m - 1) {
             const int hb = ffs64(m);   // 32 * the resetting half
-            const int er = e0 + (hb >> 5);
+            const int er2 = e0 + (hb >> 5);
             ResetLds L = reset_carve(slice, P);
             const int mr = rdl(mi, hb);
             const MapDesc md = p.maps[mr];
-            const int nc = do_reset(p, er, md, L, false);   // robot a's cell on lane a
+            const int nc = do_reset(p, er2, md, L, false);   // robot a's cell on lane a
             const int ncr = __builtin_amdgcn_ds_bpermute(ri << 2, nc);
             const bool mine = hbase == hb;
-            if (mine && act) {
-                cell = ncr;
-                carry = 0;
-                vmask = p.movevalid_cell[(uint32_t)(mvoff + ncr)];
-            }
+            if (mine && act && row0)
+                (robw + (size_t)e0 * A)[roff] = rob_pack(ncr, 0, p.movevalid_cell[(uint32_t)(mvoff + ncr)]);
             if (STALE) {
                 // every present entry of the half becomes a survivor ranked by its current key
-                uint32_t rk[NC];
+                uint32_t rk[NC], tq[NC];
 #pragma unroll
-                for (int c = 0; c < NC; c++) rk[c] = 0;
+                for (int c = 0; c < NC; c++) {
+                    rk[c] = 0;
+                    tq[c] = order_key(ps[c], c * HALF + hl);   // the key bits survive the step's updates
+                }
 #pragma unroll
                 for (int c2 = 0; c2 < NC; c2++) {
                     uint64_t pm = ballot(c2 * HALF + hl < P && (ps[c2] & PS_PRESENT)) & (0xffffffffull << hb);
@@ -500,7 +542,6 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
                 for (int c = 0; c < NC; c++) {
                     if (mine) {
                         if (c * HALF + hl < P && (ps[c] & PS_PRESENT)) {
-                            tq[c] = rk[c];
                             ps[c] = (ps[c] & PS_FLAGS) | PS_SURVIVOR | (rk[c] << PS_RANK_SHIFT);
                         } else {
                             ps[c] &= PS_STATUS;
@@ -511,55 +552,22 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 const int j = c * HALF + hl;
-                if (mine) {
-                    pk[c] = j < P ? L.pk[j] : ~0ull;
-                    ps[c] = j < P ? ((uint32_t)L.pst[j] | (STALE ? (ps[c] & ~PS_STATUS) : 0u)) : (uint32_t)ST_DELIVERED;
+                if (mine && j < P) {
+                    const uint64_t npk = L.pk[j];
+                    uint32_t nps = (uint32_t)L.pst[j] | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
                     if (STALE) {   // the update with the reset state: inserts at t = 0, nothing carried
-                        const bool ins = (j < P) & (pk_st(pk[c]) == 0) & !(ps[c] & PS_PRESENT);
-                        ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
-                        td[c] = ins ? pk[c] : td[c];
-                        dirty[c] = dirty[c] || ins;
-                        const uint32_t upd = (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
-                        ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
+                        const bool ins = (pk_st(npk) == 0) & !(nps & PS_PRESENT);
+                        nps = ins ? ((nps & PS_STATUS) | PS_PRESENT) : nps;
+                        if (ins) (trkw + eb)[(uint32_t)(h * P + j) & 0xffu] = npk;
+                        const uint32_t upd = (nps & PS_TRANSIT) ? (nps & PS_STATUS) : nps;
+                        nps = (nps & PS_PRESENT) ? upd : nps;
                     }
+                    const uint32_t o = (uint32_t)(h * P + j) & 0xffu;
+                    (pkgw + eb)[o] = npk;
+                    (pstw + eb)[o] = (uint16_t)nps;
                 }
             }
             wave_sync();   // L is read by every lane before the next half's reset rewrites it
         }
-    }
-    vmask = (((moved >> lane) & 1ull) && !do_rst) ? pvm : vmask;
-    asm volatile("" : "+v"(vmask));
-
-    // ---- outputs and write-back (pointers fetched in one late scalar batch) ----
-    GLOBAL double* rop = (GLOBAL double*)kap->r_out;
-    GLOBAL float* shp = (GLOBAL float*)kap->sh_out;
-    GLOBAL uint8_t* dnp = (GLOBAL uint8_t*)kap->done_out;
-    GLOBAL uint32_t* robw = (GLOBAL uint32_t*)kap->p.rob;
-    GLOBAL uint16_t* pstw = (GLOBAL uint16_t*)kap->p.pstate;
-    GLOBAL uint64_t* trkw = (GLOBAL uint64_t*)kap->p.trk;
-    GLOBAL uint64_t* pkgw = (GLOBAL uint64_t*)kap->p.pkg;
-    GLOBAL u32x4* esw = (GLOBAL u32x4*)kap->p.es;
-    const uint32_t er = (uint32_t)h & 1u;
-    if (live && hl == 0) {
-        if (rop) (rop + e0)[er] = rr;
-        if (shp) (shp + e0)[er] = shaped;
-        if (dnp) (dnp + e0)[er] = done ? 1 : 0;
-        (esw + e0)[er] = u32x4{(uint32_t)t_out, rfl, (uint32_t)__double2loint(total_out),
-                               (uint32_t)__double2hiint(total_out)};
-    }
-    if (live && hl == 0 && done) {
-        ((GLOBAL double*)p.ep_total + e0)[er] = total;
-        ((GLOBAL int32_t*)p.ep_len + e0)[er] = t1;
-    }
-    if (act && row0) (robw + (size_t)e0 * A)[roff] = rob_pack(cell, carry, vmask);
-    const bool rhalf = (rst >> lane) & 1ull;   // this half reset: its package table is new
-    const size_t eb = (size_t)e0 * P;
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-        const int j = c * HALF + hl;
-        const uint32_t o = (uint32_t)(h * P + j) & 0xffu;
-        if (pv[c] && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
-        if (rhalf && j < P) (pkgw + eb)[o] = pk[c];
-        if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
     }
 }

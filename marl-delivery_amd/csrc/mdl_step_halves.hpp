@@ -80,8 +80,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     const uint32_t rv_ld = (robp + (size_t)e0 * A)[roff_c];
     const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
     uint64_t pk[NC], td[NC];
-    uint32_t ps[NC];
-    uint32_t ps_in[NC / 2];   // the loaded state words, two 16-bit words per register (compared at the stores)
+    uint32_t ps[NC], ps_in[NC];
     bool dirty[NC], pv[NC];
     GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
     GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
@@ -114,8 +113,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         pk[c] = pv[c] ? pk[c] : ~0ull;
         ps[c] = pv[c] ? ps[c] : (uint32_t)ST_DELIVERED;
         td[c] = pv[c] ? td[c] : ~0ull;
-        if (c & 1) ps_in[c >> 1] |= ps[c] << 16;
-        else ps_in[c >> 1] = ps[c];
+        ps_in[c] = ps[c];
     }
     const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride;
     const int T = p.T;
@@ -143,14 +141,14 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         if (!STALE || !(ps0[c] & PS_SURVIVOR)) td[c] = pk[c];
     }
     // tracker_prev's dict-order key of slot j: a survivor's rank, else ORD_EPISODE + j (stale mode),
-    // recomputed where it is needed (registers are this kernel's occupancy limit)
+    // recomputed where it is needed rather than held in registers across the step
     auto order_key = [&](uint32_t f, int j) -> uint32_t {
         return STALE ? ((f & PS_SURVIVOR) ? (f >> PS_RANK_SHIFT) : ORD_EPISODE + (uint32_t)j) : (uint32_t)j;
     };
 
     // ---- the shaped reward's candidates (tracker_prev's waiting entries with st <= t): pre-step
-    // state only, packed now into each half's LDS list {start cell, order key << 10 | list index}
-    // (order keys are distinct, so the index only names the winner: its start cell is one LDS read) ----
+    // state only, packed now into each half's LDS list {start cell, order key << 10 | slot} ----
+    int stc[NC];
     uint64_t anyw = 0, wvm[NC];
     bool wv[NC];
 #pragma unroll
@@ -158,6 +156,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         const uint32_t f = ps0[c];
         const bool waiting = STALE ? ((f & PS_PRESENT) && !(f & PS_TRANSIT)) : ((f & PS_STATUS) == ST_WAITING);
         wv[c] = !(MDL_ABLATE & 64) && waiting && pk_st(td[c]) <= t0;
+        stc[c] = pk_start(td[c]);
         wvm[c] = ballot(wv[c]);
         anyw |= wvm[c];
     }
@@ -170,8 +169,8 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             const int idx = nh + popc64(wvm[c] & lt);
-            const uint32_t klo = (order_key(ps0[c], c * HALF + hl) << 10) | (uint32_t)idx;
-            if (wv[c]) cand[idx] = (uint64_t)(uint32_t)pk_start(td[c]) | ((uint64_t)klo << 32);
+            const uint32_t klo = (order_key(ps0[c], c * HALF + hl) << 10) | (uint32_t)(c * HALF + hl);
+            if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo << 32);
             n0 += popc64(wvm[c] & 0x00000000ffffffffull);
             n1 += popc64(wvm[c] & 0xffffffff00000000ull);
             nh = h ? n1 : n0;
@@ -379,32 +378,28 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
             // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.
             const uint64_t* cp = cand + ((lane >> 4) & 1);
             uint32_t kmin = 0xffffffffu;
-#pragma nounroll
+            uint64_t hmc = 0;
             for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
                 const uint64_t ce = cp[i0], cf = cp[i0 + 2];
                 const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
                 const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
                 kmin = min(kmin, min(ke, kf));
+                hmc |= ballot((int)(uint32_t)ce == cell) | ballot((int)(uint32_t)cf == cell);
             }
             {
                 const auto r = __builtin_amdgcn_permlane16_swap(kmin, kmin, false, false);
                 kmin = r[0] < r[1] ? r[0] : r[1];
             }
-            // "A waiting package starts at my new cell" (the can-pick-up test) matters only for agents
-            // with op 1 that carry nothing before and after the step (Mwpick below): per such robot
-            // index, one compare per package slot of its half and a ballot -- not a compare and a
-            // ballot per candidate in the scan for every agent.
-            const bool need_can = act && op == 1 && pcarry == 0 && carry == 0;
-            for (uint32_t u = rows_union(ballot(need_can)); u; u &= u - 1) {
-                const int J = __ffs((int)u) - 1;
-                const int ca = __builtin_amdgcn_ds_bpermute((rbase + J) << 2, cell);   // robot J's new cell
-                bool hit = false;
+            const uint32_t h16 = (uint32_t)(((hmc >> hbase) | (hmc >> (hbase + 16))) & 0xffffull);
+            Mcan = ((h16 >> ri) & 1u) ? ~0u : 0u;
+            const int js = (int)(kmin & 1023u);
+            const int sl = (hbase + (js & 31)) << 2;
+            int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);
 #pragma unroll
-                for (int c = 0; c < NC; c++) hit = hit | (wv[c] && pk_start(td[c]) == ca);
-                const uint64_t hm = ballot(hit);
-                Mcan = (ri == J && ((hm >> hbase) & 0xffffffffull) != 0ull) ? ~0u : Mcan;
+            for (int c = 1; c < NC; c++) {
+                const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
+                bc = (js >> 5) == c ? v : bc;
             }
-            const int bc = (int)(uint32_t)cand[kmin & 127u];   // the nearest candidate's start cell
             const bool found = act && kmin != 0xffffffffu;
             Midle = lmask(found && (kmin >> 21) <= 3u);
             best_cell = found ? bc : -1;
@@ -500,7 +495,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         const int j = c * HALF + hl;
         const uint32_t o = (uint32_t)(h * P + j) & 0xffu;
         // (dirty marks inserts of this step, which a resetting half does not make)
-        if (pv[c] && !do_rst && ps[c] != ((ps_in[c >> 1] >> (16 * (c & 1))) & 0xffffu)) (pstw + eb)[o] = (uint16_t)ps[c];
+        if (pv[c] && !do_rst && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
         if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
     }
 

@@ -82,6 +82,9 @@ __device__ __forceinline__ uint32_t tgt_dl(uint64_t v) {
 // LDS bytes per wave: the gather records (4 chunks x 64 lanes x 16 B), then the 256 flag bytes;
 // the reset scratch reuses the slice after both are consumed.
 __host__ __device__ constexpr size_t rows_scratch_bytes(int NC) { return (size_t)NC * 64 * 16 + 64 * (size_t)NC; }
+// where a resetting wave keeps its state words during the reset: the slice's last 512 bytes, past the
+// reset scratch of P <= 64 packages (reset_lds_bytes(64) = 3,712 <= 3,840)
+constexpr size_t ROWS_PS_STASH = rows_scratch_bytes(4) - 4 * 64 * 2;
 // one flag byte per package slot, a lane's NC slots in one load
 template <int NC> struct FlagWord;
 template <> struct FlagWord<4> { typedef uint32_t T; };
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     const uint32_t rv_ld = (robp + (size_t)e0 * A)[roff_c];
     const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
     uint64_t pk[NC], td[NC];
-    uint32_t ps[NC], ps_in[NC], tq[NC];
+    uint32_t ps[NC], ps_in[NC];
     bool dirty[NC];
     GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
     GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
@@ -195,15 +198,14 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     uint32_t ps0[NC];
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        const int j = c * ROW + rl;
         ps0[c] = ps[c];
-        if (!STALE || !(ps0[c] & PS_SURVIVOR)) {
-            td[c] = pk[c];
-            tq[c] = STALE ? ORD_EPISODE + (uint32_t)j : (uint32_t)j;
-        } else {
-            tq[c] = ps0[c] >> PS_RANK_SHIFT;
-        }
+        if (!STALE || !(ps0[c] & PS_SURVIVOR)) td[c] = pk[c];
     }
+    // tracker_prev's dict-order key of slot j: a survivor's rank, else ORD_EPISODE + j (stale mode),
+    // recomputed where it is needed rather than held in registers across the step
+    auto order_key = [&](uint32_t f, int j) -> uint32_t {
+        return STALE ? ((f & PS_SURVIVOR) ? (f >> PS_RANK_SHIFT) : ORD_EPISODE + (uint32_t)j) : (uint32_t)j;
+    };
 
     // ---- the shaped reward's pre-step part (MAPPO/helper.py:257-369): every agent's nearest waiting
     // package of tracker_prev, from its pre-step cell -- nothing here depends on this step's
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         const bool wv = waiting && pk_st(td[c]) <= t0;
         stc[c] = pk_start(td[c]);
         swv[c] = wv ? stc[c] : -1;
-        klo[c] = wv ? (tq[c] << 10) | (uint32_t)(c * ROW + rl) : 0xffffffffu;
+        klo[c] = wv ? (order_key(f, c * ROW + rl) << 10) | (uint32_t)(c * ROW + rl) : 0xffffffffu;
         anyw |= ballot(wv);
     }
     uint32_t Midle = 0;
@@ -479,82 +481,21 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         }
     }
 
-    // ---- reset on done (MAPPO/trainer.py:230-235): one row at a time, by the whole wave ----
-    int t_out = do_rst ? 0 : t1;
-    double total_out = do_rst ? 0.0 : total;
-    if (rst) {
-        wave_sync();   // the flag bytes and gather records are consumed (the reset scratch overlays them)
-        for (uint64_t m = rst & 0x0001000100010001ull; m; m &= m - 1) {
-            const int rb = ffs64(m);   // 16 * the resetting row
-            const int er = e0 + (rb >> 4);
-            ResetLds L = reset_carve(slice, P);
-            const int mr = rdl(mi, rb);
-            const MapDesc md = p.maps[mr];
-            const int nc = do_reset(p, er, md, L, false);   // robot a's cell on lane a
-            const int ncr = __builtin_amdgcn_ds_bpermute(rl << 2, nc);
-            const bool mine = rbase == rb;
-            if (mine && act) {
-                cell = ncr;
-                carry = 0;
-                vmask = p.movevalid_cell[(uint32_t)(mvoff + ncr)];
-            }
-            if (STALE) {
-                // every present entry of the row becomes a survivor ranked by its current key
-                uint32_t rk[NC];
-#pragma unroll
-                for (int c = 0; c < NC; c++) rk[c] = 0;
-#pragma unroll
-                for (int c2 = 0; c2 < NC; c2++) {
-                    uint64_t pm = ballot(c2 * ROW + rl < P && (ps[c2] & PS_PRESENT)) & (0xffffull << rb);
-                    while (pm) {
-                        const uint32_t ki = (uint32_t)rdl((int)tq[c2], ffs64(pm));
-                        pm &= pm - 1;
-#pragma unroll
-                        for (int c = 0; c < NC; c++) rk[c] += ki < tq[c] ? 1u : 0u;
-                    }
-                }
-#pragma unroll
-                for (int c = 0; c < NC; c++) {
-                    if (mine) {
-                        if (c * ROW + rl < P && (ps[c] & PS_PRESENT)) {
-                            tq[c] = rk[c];
-                            ps[c] = (ps[c] & PS_FLAGS) | PS_SURVIVOR | (rk[c] << PS_RANK_SHIFT);
-                        } else {
-                            ps[c] &= PS_STATUS;
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < NC; c++) {
-                const int j = c * ROW + rl;
-                if (mine) {
-                    pk[c] = j < P ? L.pk[j] : ~0ull;   // (the sentinels again past P)
-                    ps[c] = j < P ? ((uint32_t)L.pst[j] | (STALE ? (ps[c] & ~PS_STATUS) : 0u)) : (uint32_t)ST_DELIVERED;
-                    if (STALE) {   // the update with the reset state: inserts at t = 0, nothing carried
-                        const bool ins = (j < P) & (pk_st(pk[c]) == 0) & !(ps[c] & PS_PRESENT);
-                        ps[c] = ins ? ((ps[c] & PS_STATUS) | PS_PRESENT) : ps[c];
-                        td[c] = ins ? pk[c] : td[c];
-                        dirty[c] = dirty[c] || ins;
-                        const uint32_t upd = (ps[c] & PS_TRANSIT) ? (ps[c] & PS_STATUS) : ps[c];
-                        ps[c] = (ps[c] & PS_PRESENT) ? upd : ps[c];
-                    }
-                }
-            }
-            wave_sync();   // L is read by every lane before the next row's reset rewrites it
-        }
-    }
+    // ---- outputs and write-back of the step (pointers fetched in one late scalar batch, as k_step).
+    // A row that resets stores only its outputs and env record here: the reset below writes its rows
+    // after these stores, so the package registers are dead while it runs (with the reset in the
+    // middle, its path set the kernel's register count: 80 VGPRs and 26 SGPR spills, against 72 and
+    // none for the step alone) ----
+    const int t_out = do_rst ? 0 : t1;
+    const double total_out = do_rst ? 0.0 : total;
     vmask = (((moved >> lane) & 1ull) && !do_rst) ? pvm : vmask;
     asm volatile("" : "+v"(vmask));
-
-    // ---- outputs and write-back (pointers fetched in one late scalar batch, as k_step) ----
     GLOBAL double* rop = (GLOBAL double*)kap->r_out;
     GLOBAL float* shp = (GLOBAL float*)kap->sh_out;
     GLOBAL uint8_t* dnp = (GLOBAL uint8_t*)kap->done_out;
     GLOBAL uint32_t* robw = (GLOBAL uint32_t*)kap->p.rob;
     GLOBAL uint16_t* pstw = (GLOBAL uint16_t*)kap->p.pstate;
     GLOBAL uint64_t* trkw = (GLOBAL uint64_t*)kap->p.trk;
-    GLOBAL uint64_t* pkgw = (GLOBAL uint64_t*)kap->p.pkg;
     GLOBAL u32x4* esw = (GLOBAL u32x4*)kap->p.es;
     // every store: a scalar row base (env e0's) + a 32-bit lane offset, one flat predicate each
     const uint32_t er = (uint32_t)r & 3u;
@@ -569,19 +510,91 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         ((GLOBAL double*)p.ep_total + e0)[er] = total;
         ((GLOBAL int32_t*)p.ep_len + e0)[er] = t1;
     }
-    if (act) (robw + (size_t)e0 * A)[roff] = rob_pack(cell, carry, vmask);
-    const bool rrow = (rst >> lane) & 1ull;   // this row reset: its package table is new
+    if (act && !do_rst) (robw + (size_t)e0 * A)[roff] = rob_pack(cell, carry, vmask);
     const size_t eb = (size_t)e0 * P;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        const int j = c * ROW + rl;
-        const uint32_t o = (uint32_t)(r * P + j) & 0x1ffu;
+        const uint32_t o = (uint32_t)(r * P + c * ROW + rl) & 0x1ffu;
         // Every store tests the slot's existence (pv: j < P in a live row).  A sentinel slot's start
         // time 0xffff equals t1 once a done env steps on without reset to t = 65535, which "spawns"
         // it (and inserts it into the stale tracker); its masked offset then names the next env's
         // slot, or lies past the allocation for the last env.  (k_step guards its stores with j < P.)
-        if (pv[c] && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
-        if (rrow && j < P) (pkgw + eb)[o] = pk[c];
+        // dirty marks inserts of this step, which a resetting row does not make.
+        if (pv[c] && !do_rst && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
         if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
+    }
+
+    // ---- reset on done (MAPPO/trainer.py:230-235): one row at a time, by the whole wave; it writes
+    // the row's robots, package table and state words (and the tracker's t = 0 inserts) ----
+    if (rst) {
+        GLOBAL uint64_t* pkgw = (GLOBAL uint64_t*)kap->p.pkg;
+        wave_sync();   // the flag bytes and gather records are consumed (the reset scratch overlays them)
+        for (uint64_t m = rst & 0x0001000100010001ull; m; m &= m - 1) {
+            const int rb = ffs64(m);   // 16 * the resetting row
+            const int er2 = e0 + (rb >> 4);
+            const bool mine = rbase == rb;
+            if (STALE) {
+                // every present entry of the row becomes a survivor ranked by its current key
+                uint32_t rk[NC], tq[NC];
+#pragma unroll
+                for (int c = 0; c < NC; c++) {
+                    rk[c] = 0;
+                    tq[c] = order_key(ps[c], c * ROW + rl);   // the key bits survive the step's updates
+                }
+#pragma unroll
+                for (int c2 = 0; c2 < NC; c2++) {
+                    uint64_t pm = ballot(c2 * ROW + rl < P && (ps[c2] & PS_PRESENT)) & (0xffffull << rb);
+                    while (pm) {
+                        const uint32_t ki = (uint32_t)rdl((int)tq[c2], ffs64(pm));
+                        pm &= pm - 1;
+#pragma unroll
+                        for (int c = 0; c < NC; c++) rk[c] += ki < tq[c] ? 1u : 0u;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < NC; c++) {
+                    if (mine) {
+                        if (c * ROW + rl < P && (ps[c] & PS_PRESENT)) {
+                            ps[c] = (ps[c] & PS_FLAGS) | PS_SURVIVOR | (rk[c] << PS_RANK_SHIFT);
+                        } else {
+                            ps[c] &= PS_STATUS;
+                        }
+                    }
+                }
+            }
+            // the state words wait in LDS past the reset scratch while the reset runs (registers,
+            // not LDS, bound this kernel's occupancy)
+            uint16_t* pss = (uint16_t*)(slice + ROWS_PS_STASH);
+#pragma unroll
+            for (int c = 0; c < NC; c++) pss[c * 64 + lane] = (uint16_t)ps[c];
+            ResetLds L = reset_carve(slice, P);
+            const int mr = rdl(mi, rb);
+            const MapDesc md = p.maps[mr];
+            const int nc = do_reset(p, er2, md, L, false);   // robot a's cell on lane a
+            const int ncr = __builtin_amdgcn_ds_bpermute(rl << 2, nc);
+            if (mine && act)
+                (robw + (size_t)e0 * A)[roff] = rob_pack(ncr, 0, p.movevalid_cell[(uint32_t)(mvoff + ncr)]);
+#pragma unroll
+            for (int c = 0; c < NC; c++) ps[c] = pss[c * 64 + lane];
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const int j = c * ROW + rl;
+                if (mine && j < P) {
+                    const uint64_t npk = L.pk[j];
+                    uint32_t nps = (uint32_t)L.pst[j] | (STALE ? (ps[c] & ~PS_STATUS) : 0u);
+                    const uint32_t o = (uint32_t)(r * P + j) & 0x1ffu;
+                    if (STALE) {   // the update with the reset state: inserts at t = 0, nothing carried
+                        const bool ins = (pk_st(npk) == 0) & !(nps & PS_PRESENT);
+                        nps = ins ? ((nps & PS_STATUS) | PS_PRESENT) : nps;
+                        if (ins) (trkw + eb)[o] = npk;
+                        const uint32_t upd = (nps & PS_TRANSIT) ? (nps & PS_STATUS) : nps;
+                        nps = (nps & PS_PRESENT) ? upd : nps;
+                    }
+                    (pkgw + eb)[o] = npk;
+                    (pstw + eb)[o] = (uint16_t)nps;
+                }
+            }
+            wave_sync();   // L is read by every lane before the next row's reset rewrites it
+        }
     }
 }

@@ -147,7 +147,8 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     };
 
     // ---- the shaped reward's candidates (tracker_prev's waiting entries with st <= t): pre-step
-    // state only, packed now into each half's LDS list {start cell, order key << 10 | slot} ----
+    // state only, packed now into each half's LDS list {start cell, order << 7 | slot}, where the
+    // order (8 bits) is a survivor's rank (< P <= 128) or 128 + slot, in the order of order_key ----
     int stc[NC];
     uint64_t anyw = 0, wvm[NC];
     bool wv[NC];
@@ -169,16 +170,19 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             const int idx = nh + popc64(wvm[c] & lt);
-            const uint32_t klo = (order_key(ps0[c], c * HALF + hl) << 10) | (uint32_t)(c * HALF + hl);
+            const uint32_t j = (uint32_t)(c * HALF + hl);
+            const uint32_t ord = STALE ? ((ps0[c] & PS_SURVIVOR) ? (ps0[c] >> PS_RANK_SHIFT) : 128u + j) : j;
+            const uint32_t klo = (ord << 7) | j;
             if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo << 32);
             n0 += popc64(wvm[c] & 0x00000000ffffffffull);
             n1 += popc64(wvm[c] & 0xffffffff00000000ull);
             nh = h ? n1 : n0;
         }
-        // both halves scan the same (wave-uniform) count: each pads its list with sentinels (key bits
-        // ~0: never below a real key; cell ~0: no map cell) to a multiple of 4 of the longer one
+        // both halves scan the same (wave-uniform) count: each pads its list with sentinels (cell ~0:
+        // no map cell, at distance >= 510 from every cell; key bits 0xffff) to a multiple of 4 of the
+        // longer one
         nwg = (max(n0, n1) + 3) & ~3;
-        for (int k = nh + hl; k < nwg; k += HALF) cand[k] = ~0ull;
+        for (int k = nh + hl; k < nwg; k += HALF) cand[k] = 0x0000ffffffffffffull;
     }
 
     // ---- the pre-step carried package of each robot, through LDS; the flag bytes cleared ----
@@ -375,14 +379,16 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
         if (anyw && !(MDL_ABLATE & 32)) {
             // The two rows of a half scan alternate candidates for the same agent (two per step, two
             // LDS reads in flight): nearest key from the pre-step cell, and "a waiting package starts
-            // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.
+            // at my new cell" (can-pick-up) into a lane mask; one swap joins the rows.  The key is one
+            // v_sad_hi_u8: distance << 16 + (order << 7 | slot); a real distance is <= 508 (cells
+            // are row << 8 | column, both < 255), a sentinel's >= 510.
             const uint64_t* cp = cand + ((lane >> 4) & 1);
             uint32_t kmin = 0xffffffffu;
             uint64_t hmc = 0;
             for (int i0 = 0; i0 < nwg; i0 += 4) {   // wave-uniform trip count
                 const uint64_t ce = cp[i0], cf = cp[i0 + 2];
-                const uint32_t ke = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)ce) << 21) | (uint32_t)(ce >> 32);
-                const uint32_t kf = ((uint32_t)manhattan_sad(pcell, (int)(uint32_t)cf) << 21) | (uint32_t)(cf >> 32);
+                const uint32_t ke = __builtin_amdgcn_sad_hi_u8((uint32_t)pcell, (uint32_t)ce, (uint32_t)(ce >> 32));
+                const uint32_t kf = __builtin_amdgcn_sad_hi_u8((uint32_t)pcell, (uint32_t)cf, (uint32_t)(cf >> 32));
                 kmin = min(kmin, min(ke, kf));
                 hmc |= ballot((int)(uint32_t)ce == cell) | ballot((int)(uint32_t)cf == cell);
             }
@@ -392,7 +398,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
             }
             const uint32_t h16 = (uint32_t)(((hmc >> hbase) | (hmc >> (hbase + 16))) & 0xffffull);
             Mcan = ((h16 >> ri) & 1u) ? ~0u : 0u;
-            const int js = (int)(kmin & 1023u);
+            const int js = (int)(kmin & 127u);
             const int sl = (hbase + (js & 31)) << 2;
             int bc = __builtin_amdgcn_ds_bpermute(sl, stc[0]);
 #pragma unroll
@@ -400,8 +406,8 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
                 const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
                 bc = (js >> 5) == c ? v : bc;
             }
-            const bool found = act && kmin != 0xffffffffu;
-            Midle = lmask(found && (kmin >> 21) <= 3u);
+            const bool found = act && kmin < (509u << 16);
+            Midle = lmask(found && (kmin >> 16) <= 3u);
             best_cell = found ? bc : -1;
         }
         float cs[9];

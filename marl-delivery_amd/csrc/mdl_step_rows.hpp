@@ -211,10 +211,12 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     // package of tracker_prev, from its pre-step cell -- nothing here depends on this step's
     // movement or package actions, so these in-row minima are issued first and run alongside
     // those dependent chains.  Computed for all AU agents of all four rows (the terms below mask
-    // the agents that do not need it); key = distance << 21 | order key << 10 | slot (the
-    // reference's tie-break). ----
+    // the agents that do not need it); key = distance << 16 + (order << 7 | slot) in one
+    // v_sad_hi_u8, the order (7 bits) a survivor's rank (< P <= 64) or 64 + slot as order_key ranks
+    // them (the reference's tie-break); a real distance is <= 508 (cells are row << 8 | column, both
+    // < 255), a non-candidate's (cell ~0) >= 510. ----
     int stc[NC], swv[NC];
-    uint32_t klo[NC];   // order key << 10 | row-local slot, or ~0 for no candidate
+    uint32_t klo[NC];   // order << 7 | row-local slot, or 0xffff for no candidate
     uint64_t anyw = 0;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
@@ -223,7 +225,9 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         const bool wv = waiting && pk_st(td[c]) <= t0;
         stc[c] = pk_start(td[c]);
         swv[c] = wv ? stc[c] : -1;
-        klo[c] = wv ? (order_key(f, c * ROW + rl) << 10) | (uint32_t)(c * ROW + rl) : 0xffffffffu;
+        const uint32_t j = (uint32_t)(c * ROW + rl);
+        const uint32_t ord = STALE ? ((f & PS_SURVIVOR) ? (f >> PS_RANK_SHIFT) : 64u + j) : j;
+        klo[c] = wv ? (ord << 7) | j : 0xffffu;
         anyw |= ballot(wv);
     }
     uint32_t Midle = 0;
@@ -235,7 +239,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
         const int pa = row_bcast<J>(cell);                                                           \
         uint32_t k = 0xffffffffu;                                                                    \
         _Pragma("unroll") for (int c = 0; c < NC; c++) {                                             \
-            const uint32_t kc = ((uint32_t)manhattan_sad(pa, stc[c]) << 21) | klo[c];                \
+            const uint32_t kc = __builtin_amdgcn_sad_hi_u8((uint32_t)pa, (uint32_t)swv[c], klo[c]);   \
             k = kc < k ? kc : k;                                                                     \
         }                                                                                            \
         k = row_min_u32(k);                                                                          \
@@ -251,8 +255,8 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
             const int v = __builtin_amdgcn_ds_bpermute(sl, stc[c]);
             bc = (js >> 4) == c ? v : bc;
         }
-        const bool found = act && kmin != 0xffffffffu;
-        Midle = lmask(found && (kmin >> 21) <= 3u);
+        const bool found = act && kmin < (509u << 16);
+        Midle = lmask(found && (kmin >> 16) <= 3u);
         best_cell = found ? bc : -1;
     }
 

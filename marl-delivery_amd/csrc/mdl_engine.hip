@@ -109,6 +109,9 @@ int waves_per_block(size_t lds_per_wave) {
     return (int)w;
 }
 
+// elements of padding after the package table, state words and tracker (see mdl_create)
+constexpr size_t PKG_PAD = 256;
+
 }  // namespace
 
 struct MdlEngine {
@@ -404,12 +407,14 @@ int mdl_create(const MdlConfig* cfg, const uint8_t* grids, const int32_t* map_hw
     rc |= eng->alloc(&d_recip, recip.size());
     if (env_map) rc |= eng->alloc(&d_em, E);
     rc |= eng->alloc(&p.rob, E * A);
-    rc |= eng->alloc(&p.pkg, E * P);
-    rc |= eng->alloc(&p.pstate, E * P);
+    // the package buffers end in 256 slots of padding: the multi-env step kernels load every lane's
+    // slot past an env's P without clamping (k_step_halves: up to the last env's slot 127)
+    rc |= eng->alloc(&p.pkg, E * P + PKG_PAD);
+    rc |= eng->alloc(&p.pstate, E * P + PKG_PAD);
     rc |= eng->alloc(&p.es, E);
     rc |= eng->alloc(&p.mt, E * mdl::MT_N);
     rc |= eng->alloc(&p.mt_pos, E);
-    rc |= eng->alloc(&p.trk, (p.stale ? E : 1) * P);
+    rc |= eng->alloc(&p.trk, (p.stale ? E : 1) * P + PKG_PAD);
     rc |= eng->alloc(&p.ep_total, E);
     rc |= eng->alloc(&p.ep_len, E);
     if (rc) {

@@ -1839,8 +1839,11 @@ hipError_t launch_step_halves(const DevParams& p, const uint8_t* actions, int fm
     for (int k = 0; k < p.n_maps; k++) small = small && p.maps[k].H <= 64 && p.maps[k].W <= 64;
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u) | (small ? NW_SMALLMAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a
-    if (p.stale) hipLaunchKernelGGL((k_step_halves<true>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
-    else hipLaunchKernelGGL((k_step_halves<false>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    const bool full3 = p.P >= 3 * HALF;
+    if (p.stale && full3) hipLaunchKernelGGL((k_step_halves<true, 3>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    else if (p.stale) hipLaunchKernelGGL((k_step_halves<true, 0>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    else if (full3) hipLaunchKernelGGL((k_step_halves<false, 3>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
+    else hipLaunchKernelGGL((k_step_halves<false, 0>), grid, block, lds * wpb, s, MDL_STEP_ARGS);
 #undef MDL_STEP_ARGS
     return hipGetLastError();
 }
@@ -1882,7 +1885,7 @@ hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt,
 int step_kernel_name(const DevParams& p, int envs_per_wave, bool obs, char* out, int cap) {
     const char* st = p.stale ? "true" : "false";
     if (envs_per_wave == 4) return snprintf(out, (size_t)cap, "mdl::k_step_rows<%s, %d, 4>", st, p.A == 5 ? 5 : 8);
-    if (envs_per_wave == 2) return snprintf(out, (size_t)cap, "mdl::k_step_halves<%s>", st);
+    if (envs_per_wave == 2) return snprintf(out, (size_t)cap, "mdl::k_step_halves<%s, %d>", st, p.P >= 3 * HALF ? 3 : 0);
     if (obs) return snprintf(out, (size_t)cap, "mdl::k_step_obs<%s, %d>", st, p.A == 5 ? 5 : 8);
     const int nch = nch_for(p.P);
     const int au = (nch <= 2 && p.A == 5) ? 5 : (nch <= 2 && p.A == 16) ? 16 : p.A <= 8 ? 8 : 0;

@@ -41,7 +41,9 @@ __host__ __device__ constexpr size_t halves_scratch_bytes() {
     return HALF_GREC + HALF_GPS + 64 * (size_t)HALF_NC + 2 * (size_t)HALF_CAND * 8;
 }
 
-template <bool STALE>
+// NFULL: package chunks known to be full (slot c * 32 + 31 < P for c < NFULL; 3 when P >= 96): their
+// slots need no "no package" handling.
+template <bool STALE, int NFULL>
 __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict__ rob_pre,
                                                      const uint64_t* __restrict__ pkg_pre,
                                                      const uint16_t* __restrict__ pst_pre,
@@ -70,11 +72,15 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     if (wave >= wpb_ || e0 >= n_) return;
     const int h = lane >> 5, hl = lane & 31, hbase = lane & 32, rbase = lane & 48;
     const int ri = lane & 15;                // the robot this lane holds (on both rows of the half)
-    const bool live = e0 + h < n_;           // the last wave's second half past n holds no env
+    const bool live = e0 + h < n_;           // the last wave's second half past n holds no env ...
+    const int hh = live ? h : 0;             // ... and reads env e0 (it stores nothing)
     const bool act = live && ri < A;
     const bool row0 = (lane & 16) == 0;      // the robot copy that stores
 
-    // ---- loads: one round trip, every lane loads (in-bounds offsets, discarded where unused) ----
+    // ---- loads: one round trip, every lane loads (in-bounds offsets, discarded where unused).  Slot
+    // j = c * 32 + hl of env e0 + hh is element lb + 32 c (lb < 160: the chunks' byte offsets fold
+    // into the loads' immediates); lanes past P read the next env's slots or the 256-slot tail
+    // padding of the package buffers (MdlEngine) ----
     const uint32_t roff = (uint32_t)(h * A + ri);
     const uint32_t roff_c = (act ? roff : 0u) & 0x1fu;   // h * A + ri < 32
     const uint32_t rv_ld = (robp + (size_t)e0 * A)[roff_c];
@@ -85,17 +91,16 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
     GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
     GLOBAL const uint64_t* trke = trkp + (size_t)e0 * P;
+    const uint32_t lb = (uint32_t)(hh * P + hl) & 0xffu;   // hh * P + hl < 160
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        const int j = c * HALF + hl;
-        pv[c] = live && j < P;
-        const uint32_t o = (pv[c] ? (uint32_t)(h * P + j) : 0u) & 0xffu;   // h * P + j < 256
-        pk[c] = pkge[o];
-        ps[c] = pste[o];
-        td[c] = STALE ? trke[o] : 0ull;
+        pv[c] = c < NFULL || c * HALF + hl < P;
+        pk[c] = pkge[lb + c * HALF];
+        ps[c] = pste[lb + c * HALF];
+        td[c] = STALE ? trke[lb + c * HALF] : 0ull;
         dirty[c] = false;
     }
-    const uint32_t erow = (uint32_t)(live ? h : 0) & 1u;
+    const uint32_t erow = (uint32_t)hh & 1u;
     const uint32_t t_ld = ((GLOBAL const uint32_t*)(esp + e0))[4u * erow];
     const uint64_t tot_ld = ((GLOBAL const uint64_t*)(esp + e0))[2u * erow + 1u];
     KargPtr kap = (KargPtr)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
@@ -104,15 +109,17 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any use
     const uint32_t rv = act ? rv_ld : 0u;
     int araw = act ? (int)(ar_ld & 0xffu) : 0;
-    const uint32_t t_rec = live ? t_ld : 0u;
-    const uint64_t tot_rec = live ? tot_ld : 0ull;
+    const uint32_t t_rec = t_ld;
+    const uint64_t tot_rec = tot_ld;
     // slots without a package: the sentinels of k_step_rows (status delivered, start time and
-    // start cell 0xffff); every store below tests pv
+    // start cell 0xffff); every store below tests pv (and live)
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        pk[c] = pv[c] ? pk[c] : ~0ull;
-        ps[c] = pv[c] ? ps[c] : (uint32_t)ST_DELIVERED;
-        td[c] = pv[c] ? td[c] : ~0ull;
+        if (c >= NFULL) {
+            pk[c] = pv[c] ? pk[c] : ~0ull;
+            ps[c] = pv[c] ? ps[c] : (uint32_t)ST_DELIVERED;
+            td[c] = pv[c] ? td[c] : ~0ull;
+        }
         ps_in[c] = ps[c];
     }
     const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride;
@@ -121,7 +128,7 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     int mvoff = p.maps[0].mvc_off;
     int mi = 0;
     if (nw & NW_MAP) {   // mixed maps: each half's map
-        mi = (int)((GLOBAL const uint8_t*)p.env_map)[e0 + (live ? h : 0)];
+        mi = (int)((GLOBAL const uint8_t*)p.env_map)[e0 + hh];
 #pragma unroll
         for (int k = 1; k < MAX_MAPS; k++) mvoff = (mi == k) ? p.maps[k].mvc_off : mvoff;
     }
@@ -164,20 +171,23 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     uint64_t* cand = (uint64_t*)(slice + HALF_GREC + HALF_GPS + 64 * NC) + h * HALF_CAND;   // this lane's half
     int nwg = 0;
     if (anyw) {
-        const uint64_t hm = h ? 0xffffffff00000000ull : 0x00000000ffffffffull;
-        const uint64_t lt = lanemask_lt() & hm;
-        int n0 = 0, n1 = 0, nh = 0;
+        // list position: the candidates below this lane in the whole wave (v_mbcnt), less half 0's
+        // in half 1, plus the half's earlier chunks
+        int n0 = 0, n1 = 0;
 #pragma unroll
         for (int c = 0; c < NC; c++) {
-            const int idx = nh + popc64(wvm[c] & lt);
+            const int lo = popc64(wvm[c] & 0x00000000ffffffffull);
+            const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(wvm[c] >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)wvm[c], 0u));
+            const int idx = below + (h ? n1 - lo : n0);
             const uint32_t j = (uint32_t)(c * HALF + hl);
             const uint32_t ord = STALE ? ((ps0[c] & PS_SURVIVOR) ? (ps0[c] >> PS_RANK_SHIFT) : 128u + j) : j;
             const uint32_t klo = (ord << 7) | j;
             if (wv[c]) cand[idx] = (uint64_t)(uint32_t)stc[c] | ((uint64_t)klo << 32);
-            n0 += popc64(wvm[c] & 0x00000000ffffffffull);
+            n0 += lo;
             n1 += popc64(wvm[c] & 0xffffffff00000000ull);
-            nh = h ? n1 : n0;
         }
+        const int nh = h ? n1 : n0;
         // both halves scan the same (wave-uniform) count: each pads its list with sentinels (cell ~0:
         // no map cell, at distance >= 510 from every cell; key bits 0xffff) to a multiple of 4 of the
         // longer one
@@ -266,22 +276,21 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
             // Every map within 64 x 64: each half's pickers mark their cells in a 4096-bit map in LDS
             // (over the gather records, consumed before the movement); a waiting package tests one
             // bit, and the few packages under a picker are assigned in index order by the scalar
-            // unit -- the first one at a picker's cell is its lowest-index package.
-            uint32_t* pb = (uint32_t*)slice;
-            auto bit_of = [](int cl) { return ((cl & 63) << 6) | ((cl >> 8) & 63); };
+            // unit -- the first one at a picker's cell is its lowest-index package.  Cell
+            // row << 8 | column is bit column & 31 of word 2 row + column / 32.
+            uint32_t* pb = (uint32_t*)slice + h * 128;
+            auto word_of = [](int cl) { return (((uint32_t)cl >> 7) | (((uint32_t)cl >> 5) & 1u)) & 127u; };
             wave_sync();
-            reinterpret_cast<u32x4*>(pb)[lane] = u32x4{0u, 0u, 0u, 0u};   // both halves' maps: 1 KB
+            reinterpret_cast<u32x4*>((uint32_t*)slice)[lane] = u32x4{0u, 0u, 0u, 0u};   // both halves' maps: 1 KB
             wave_sync();
-            if (picker && row0) {
-                const int ix = bit_of(cell);
-                atomicOr(&pb[h * 128 + (ix >> 5)], 1u << (ix & 31));
-            }
+            if (picker && row0) atomicOr(&pb[word_of(cell)], 1u << (cell & 31));
             wave_sync();
             uint64_t left = pickers & 0x0000ffff0000ffffull;   // row 0's robot copies
 #pragma unroll
             for (int c = 0; c < NC; c++) {
-                const int ix = bit_of(sw[c]);   // sw < 0: some in-range bit, masked
-                const uint64_t mt = ballot(sw[c] >= 0 && ((pb[h * 128 + (ix >> 5)] >> (ix & 31)) & 1u));
+                // sw < 0: some in-range word, masked (no short-circuit: no branch per chunk)
+                const uint32_t bit = __builtin_amdgcn_ubfe(pb[word_of(sw[c])], (uint32_t)sw[c] & 31u, 1u);
+                const uint64_t mt = ballot((sw[c] >= 0) & (bit != 0u));
                 for (uint64_t m = mt; m && left; m &= m - 1) {
                     const int j = ffs64(m);
                     const uint64_t who = ballot(cell == rdl(sw[c], j)) & left & (0xffffull << (j & 32));
@@ -498,11 +507,10 @@ __global__ __launch_bounds__(256) void k_step_halves(const uint32_t* __restrict_
     const size_t eb = (size_t)e0 * P;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        const int j = c * HALF + hl;
-        const uint32_t o = (uint32_t)(h * P + j) & 0xffu;
+        const uint32_t o = lb + c * HALF;
         // (dirty marks inserts of this step, which a resetting half does not make)
-        if (pv[c] && !do_rst && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
-        if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
+        if (live && pv[c] && !do_rst && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
+        if (STALE && live && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
     }
 
     // ---- reset on done (MAPPO/trainer.py:230-235): one half at a time, by the whole wave; it writes

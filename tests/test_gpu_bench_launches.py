@@ -12,7 +12,7 @@ item 1).
   65,536 envs of map1..map5 (contiguous map groups, seeds 42 + global id).  Here that batch runs 45
   steps across an auto-reset with oracle windows at the start, at every map-group boundary
   (13,108, 26,215, 39,322, 52,429) and at the last wave; state, tracker rows and vectors at the end.
-* Config 5: ``bench.py --config 5`` at one GPU times ONE ``k_step_halves<true>`` launch over 131,072
+* Config 5: ``bench.py --config 5`` at one GPU times ONE ``k_step_halves<true, 3>`` launch over 131,072
   envs (64x64, 16 robots, 100 packages); the same batch runs 45 steps across an auto-reset with
   oracle windows at the start, the middle, an XCD-slot boundary and the last wave.
 * The tests assert which kernel the engine launched (``mdl_last_step_layout`` /
@@ -129,7 +129,7 @@ def test_config4_rows_65536_five_maps_vs_oracle():
 
 
 def test_config5_halves_131072_vs_oracle():
-    """Config 5 at one GPU: ``bench.py --config 5`` times ONE ``k_step_halves<true>`` launch over
+    """Config 5 at one GPU: ``bench.py --config 5`` times ONE ``k_step_halves<true, 3>`` launch over
     131,072 envs of the 64x64 map (16 robots, 100 packages; the layout AUTO takes there).  Here that
     batch runs 45 steps across an auto-reset (T = 30) with oracle windows at the start, around the
     middle, at an XCD-slot boundary and at the last wave: rewards, shaped rewards and dones every
@@ -140,7 +140,7 @@ def test_config5_halves_131072_vs_oracle():
     env = mg.BatchedEnv(g, E, A, P, T, seed=42, tracker="mappo", shaping="mappo", max_other_robots=15,
                         max_packages_obs=20, max_robots_state=16, max_packages_state=100)
     env.reset()
-    assert env.step_layout() == "halves" and env.step_kernel_name() == "mdl::k_step_halves<true>"
+    assert env.step_layout() == "halves" and env.step_kernel_name() == "mdl::k_step_halves<true, 3>"
     starts = [0, 16381, 65533, 98304 - 3, E - W]
     wins = [(s, O.OracleBatch(W, g, A, P, T, seed_base=42 + s, clear_on_reset=False)) for s in starts]
     gen = np.random.RandomState(55)

@@ -1869,13 +1869,16 @@ hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt,
     const uint32_t ap = pack_ap(p.A, p.P, (int)grid.x);
     const uint32_t nw = (uint32_t)n | ((uint32_t)wpb << 24) | (p.env_map ? NW_MAP : 0u);
 #define MDL_STEP_ARGS p.rob, p.pkg, p.pstate, (const u32x4*)p.es, p.trk, actions, ap, nw, a
-#define MDL_ROWS(ST, NC)                                                                                  \
-    do {                                                                                                  \
-        if (p.A == 5) hipLaunchKernelGGL((k_step_rows<ST, 5, NC>), grid, block, lds * wpb, s, MDL_STEP_ARGS);   \
-        else hipLaunchKernelGGL((k_step_rows<ST, 8, NC>), grid, block, lds * wpb, s, MDL_STEP_ARGS);      \
+#define MDL_ROWS(ST, NF)                                                                                     \
+    do {                                                                                                     \
+        if (p.A == 5) hipLaunchKernelGGL((k_step_rows<ST, 5, 4, NF>), grid, block, lds * wpb, s, MDL_STEP_ARGS);   \
+        else hipLaunchKernelGGL((k_step_rows<ST, 8, 4, NF>), grid, block, lds * wpb, s, MDL_STEP_ARGS);      \
     } while (0)
-    if (p.stale) MDL_ROWS(true, 4);
-    else MDL_ROWS(false, 4);
+    const bool full3 = p.P >= 3 * ROW;
+    if (p.stale && full3) MDL_ROWS(true, 3);
+    else if (p.stale) MDL_ROWS(true, 0);
+    else if (full3) MDL_ROWS(false, 3);
+    else MDL_ROWS(false, 0);
 #undef MDL_ROWS
 #undef MDL_STEP_ARGS
     return hipGetLastError();
@@ -1884,7 +1887,8 @@ hipError_t launch_step_rows(const DevParams& p, const uint8_t* actions, int fmt,
 // (the dispatch of launch_step_rows / launch_step_halves above, launch_step_obs and launch_step_t below)
 int step_kernel_name(const DevParams& p, int envs_per_wave, bool obs, char* out, int cap) {
     const char* st = p.stale ? "true" : "false";
-    if (envs_per_wave == 4) return snprintf(out, (size_t)cap, "mdl::k_step_rows<%s, %d, 4>", st, p.A == 5 ? 5 : 8);
+    if (envs_per_wave == 4)
+        return snprintf(out, (size_t)cap, "mdl::k_step_rows<%s, %d, 4, %d>", st, p.A == 5 ? 5 : 8, p.P >= 3 * ROW ? 3 : 0);
     if (envs_per_wave == 2) return snprintf(out, (size_t)cap, "mdl::k_step_halves<%s, %d>", st, p.P >= 3 * HALF ? 3 : 0);
     if (obs) return snprintf(out, (size_t)cap, "mdl::k_step_obs<%s, %d>", st, p.A == 5 ? 5 : 8);
     const int nch = nch_for(p.P);

@@ -91,7 +91,9 @@ template <> struct FlagWord<4> { typedef uint32_t T; };
 
 // (93 VGPRs, 5 waves per SIMD.  Capping it at 6 waves (79 VGPRs) was 1 % faster on config 4 and 3-6 %
 // slower at 4,096-16,384 envs, at 7 waves 20 % slower: profiles/r05/rows_ab.txt.)
-template <bool STALE, int AU, int NC>
+// NFULL: package chunks known to be full (slot c * 16 + 15 < P for c < NFULL; 3 when P >= 48): their
+// slots need no "no package" handling.
+template <bool STALE, int AU, int NC, int NFULL>
 __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ rob_pre,
                                                    const uint64_t* __restrict__ pkg_pre,
                                                    const uint16_t* __restrict__ pst_pre,
@@ -120,15 +122,19 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     const int e0 = 4 * w;   // this wave's envs: e0 .. e0 + 3
     if (wave >= wpb_ || e0 >= n_) return;
     const int r = lane >> 4, rl = lane & 15, rbase = lane & 48;
-    const bool live = e0 + r < n_;   // the last wave's rows past n hold no env
+    const bool live = e0 + r < n_;   // the last wave's rows past n hold no env ...
+    const int re = live ? r : 0;     // ... and read env e0 (they store nothing)
     const bool act = live && rl < A;
 
     // ---- loads: one round trip, everything independent.  No exec-masked load blocks: every lane
     // loads (lanes without data read an in-bounds word of env e0 and discard it), so the loads
     // issue back to back with no branch and no wait between them. ----
     const uint32_t roff = (uint32_t)(r * A + rl);
-    // (offsets masked to their range -- r * A + rl < 64, r * P + j < 512 -- so the loads take the
-    // scalar-base + 32-bit-offset form instead of a 64-bit address per lane)
+    // (offsets masked to their range -- r * A + rl < 64, re * P + rl < 256 -- so the loads take the
+    // scalar-base + 32-bit-offset form instead of a 64-bit address per lane; slot j = c * 16 + rl of
+    // env e0 + re is element lb + 16 c, the chunks' byte offsets folded into the loads' immediates,
+    // and lanes past P read the next env's slots or the 256-slot tail padding of the package
+    // buffers, MdlEngine)
     const uint32_t roff_c = (act ? roff : 0u) & 0x3fu;
     const uint32_t rv_ld = (robp + (size_t)e0 * A)[roff_c];
     const uint32_t ar_ld = (actp + (size_t)e0 * A)[roff_c];
@@ -138,20 +144,19 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     GLOBAL const uint64_t* pkge = pkgp + (size_t)e0 * P;
     GLOBAL const uint16_t* pste = pstp + (size_t)e0 * P;
     GLOBAL const uint64_t* trke = trkp + (size_t)e0 * P;
-    bool pv[NC];   // package slot c * 16 + rl of this row exists
+    bool pv[NC];   // package slot c * 16 + rl of this row's env exists (the stores also test live)
+    const uint32_t lb = (uint32_t)(re * P + rl) & 0xffu;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        const int j = c * ROW + rl;
-        pv[c] = live && j < P;
-        const uint32_t o = (pv[c] ? (uint32_t)(r * P + j) : 0u) & 0x1ffu;
-        pk[c] = pkge[o];
-        ps[c] = pste[o];
-        td[c] = STALE ? trke[o] : 0ull;
+        pv[c] = c < NFULL || c * ROW + rl < P;
+        pk[c] = pkge[lb + c * ROW];
+        ps[c] = pste[lb + c * ROW];
+        td[c] = STALE ? trke[lb + c * ROW] : 0ull;
         dirty[c] = false;
     }
     // the env record's clock and total (its reward-term word is only written): two loads, so no
     // register of an unused component is recycled under a load still in flight (a forced wait)
-    const uint32_t erow = (uint32_t)(live ? r : 0) & 3u;
+    const uint32_t erow = (uint32_t)re & 3u;
     const uint32_t t_ld = ((GLOBAL const uint32_t*)(esp + e0))[4u * erow];
     const uint64_t tot_ld = ((GLOBAL const uint64_t*)(esp + e0))[2u * erow + 1u];
     // cost_fold[k] on row lane k (k <= A <= 8): the move-cost fold of the row's n_cost movers, fetched
@@ -162,8 +167,8 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any use
     const uint32_t rv = act ? rv_ld : 0u;
     int araw = act ? (int)(ar_ld & 0xffu) : 0;
-    const uint32_t t_rec = live ? t_ld : 0u;
-    const uint64_t tot_rec = live ? tot_ld : 0ull;
+    const uint32_t t_rec = t_ld;
+    const uint64_t tot_rec = tot_ld;
     // Slots without a package (j >= P, or a row past n) hold sentinels that fail every test by
     // themselves, so only the loads and the stores test the slot's existence: status delivered (the
     // all-delivered test passes over them; not waiting, not present), start time 0xffff (no spawn
@@ -171,9 +176,11 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     // memory), start cell 0xffff (no cell of a map of at most 255 rows).
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        pk[c] = pv[c] ? pk[c] : ~0ull;
-        ps[c] = pv[c] ? ps[c] : (uint32_t)ST_DELIVERED;
-        td[c] = pv[c] ? td[c] : ~0ull;
+        if (c >= NFULL) {
+            pk[c] = pv[c] ? pk[c] : ~0ull;
+            ps[c] = pv[c] ? ps[c] : (uint32_t)ST_DELIVERED;
+            td[c] = pv[c] ? td[c] : ~0ull;
+        }
         ps_in[c] = ps[c];
     }
     const int fmt = args.fmt, auto_reset = args.auto_reset, lds_stride = args.lds_stride;
@@ -182,7 +189,7 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     int mvoff = p.maps[0].mvc_off;
     int mi = 0;
     if (nw & NW_MAP) {   // mixed maps: each row's map, its move-validity table by a select chain
-        mi = (int)((GLOBAL const uint8_t*)p.env_map)[e0 + (live ? r : 0)];
+        mi = (int)((GLOBAL const uint8_t*)p.env_map)[e0 + re];
 #pragma unroll
         for (int k = 1; k < MAX_MAPS; k++) mvoff = (mi == k) ? p.maps[k].mvc_off : mvoff;
     }
@@ -518,14 +525,14 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
     const size_t eb = (size_t)e0 * P;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-        const uint32_t o = (uint32_t)(r * P + c * ROW + rl) & 0x1ffu;
+        const uint32_t o = lb + c * ROW;
         // Every store tests the slot's existence (pv: j < P in a live row).  A sentinel slot's start
         // time 0xffff equals t1 once a done env steps on without reset to t = 65535, which "spawns"
         // it (and inserts it into the stale tracker); its masked offset then names the next env's
         // slot, or lies past the allocation for the last env.  (k_step guards its stores with j < P.)
         // dirty marks inserts of this step, which a resetting row does not make.
-        if (pv[c] && !do_rst && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
-        if (STALE && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
+        if (live && pv[c] && !do_rst && ps[c] != ps_in[c]) (pstw + eb)[o] = (uint16_t)ps[c];
+        if (STALE && live && pv[c] && dirty[c]) (trkw + eb)[o] = td[c];
     }
 
     // ---- reset on done (MAPPO/trainer.py:230-235): one row at a time, by the whole wave; it writes
@@ -572,12 +579,13 @@ __global__ __launch_bounds__(256) void k_step_rows(const uint32_t* __restrict__ 
 #pragma unroll
             for (int c = 0; c < NC; c++) pss[c * 64 + lane] = (uint16_t)ps[c];
             ResetLds L = reset_carve(slice, P);
-            const int mr = rdl(mi, rb);
+            // the row's map by a scalar load (no per-lane map registers live across the reset)
+            const int mr = (nw & NW_MAP) ? (int)((GLOBAL const uint8_t*)p.env_map)[er2] : 0;
             const MapDesc md = p.maps[mr];
             const int nc = do_reset(p, er2, md, L, false);   // robot a's cell on lane a
             const int ncr = __builtin_amdgcn_ds_bpermute(rl << 2, nc);
             if (mine && act)
-                (robw + (size_t)e0 * A)[roff] = rob_pack(ncr, 0, p.movevalid_cell[(uint32_t)(mvoff + ncr)]);
+                (robw + (size_t)e0 * A)[roff] = rob_pack(ncr, 0, p.movevalid_cell[(uint32_t)(md.mvc_off + ncr)]);
 #pragma unroll
             for (int c = 0; c < NC; c++) ps[c] = pss[c * 64 + lane];
 #pragma unroll

@@ -8,7 +8,7 @@ item 1).
   across an auto-reset (T = 30); 16 envs spread over workgroups and XCD slots (2,048-env slot
   ranges) are replayed by the oracle from their seeds: rewards, shaped rewards and dones every
   step, all four observation tensors every step.
-* Config 4: ``bench.py --config 4`` at one GPU times ONE ``k_step_rows<true, 5, 4>`` launch over
+* Config 4: ``bench.py --config 4`` at one GPU times ONE ``k_step_rows<true, 5, 4, 3>`` launch over
   65,536 envs of map1..map5 (contiguous map groups, seeds 42 + global id).  Here that batch runs 45
   steps across an auto-reset with oracle windows at the start, at every map-group boundary
   (13,108, 26,215, 39,322, 52,429) and at the last wave; state, tracker rows and vectors at the end.
@@ -84,7 +84,7 @@ def test_config4_rows_65536_five_maps_vs_oracle():
     env = mg.BatchedEnv(grids, total, A, P, T, seeds=seeds, env_map=env_map, tracker="mappo", shaping="mappo",
                         max_packages_obs=5)
     env.reset()
-    assert env.step_layout() == "rows" and env.step_kernel_name() == "mdl::k_step_rows<true, 5, 4>"
+    assert env.step_layout() == "rows" and env.step_kernel_name() == "mdl::k_step_rows<true, 5, 4, 3>"
     # windows inside one map group each: the first envs, both sides of every group boundary, the last wave
     wins = [(0, 0)]
     for m in range(1, 5):

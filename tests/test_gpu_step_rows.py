@@ -3,7 +3,7 @@ one-env-per-wavefront step (k_step, "wave"): same seeds, same actions, every out
 engine state (save_state: robots, packages, statuses, tracker, per-env scalars and reward-term bits,
 RNG words, episode records) bit for bit after every step -- across auto-resets, in both tracker
 modes, both action formats, A < 5 / A = 5 / A = 8 (numpy's 8-partial sum), P from 1 to 64 (the four package chunks per lane of the
-only instantiated form, k_step_rows<.., .., 4>), env counts that leave the last wave's rows empty, mixed
+only instantiated form, k_step_rows<.., .., 4, ..>), env counts that leave the last wave's rows empty, mixed
 maps, and a done env stepped on without reset past t = 0xffff (the sentinel slots' start time).
 The oracle and golden-fixture tests run this kernel too (test_gpu_parity.py: test_vs_oracle_rows_layout,
 the "rows" cases of test_vs_oracle_map1 and test_mappo_rollout_golden); the default layout ("auto")
@@ -128,7 +128,7 @@ def test_rows_auto_threshold():
     assert small.step_layout() == "wave" and big.step_layout() == "rows"
     assert big.step_layout(n=7168) == "wave"   # an env_ids subset: always one wave per env
     assert big.last_step_layout() is None
-    assert big.step_kernel_name() == "mdl::k_step_rows<true, 5, 4>"
+    assert big.step_kernel_name() == "mdl::k_step_rows<true, 5, 4, 3>"
     assert small.step_kernel_name() == "mdl::k_step<true, 1, false, 5>"
     ref = mg.BatchedEnv(grid("map1.txt"), 7168, 5, 50, 30, seed=1, step_layout="wave")
     for e in (big, ref, small):

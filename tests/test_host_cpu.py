@@ -251,7 +251,8 @@ def _kernel_resources(so_path, tmp_path):
                 if len(t) == 2 and t[0] == ".name:":
                     name = t[1]
                     res[name] = {}
-                elif name and len(t) == 2 and t[0] in (".private_segment_fixed_size:", ".sgpr_count:", ".vgpr_count:"):
+                elif name and len(t) == 2 and t[0] in (".private_segment_fixed_size:", ".sgpr_count:", ".sgpr_spill_count:",
+                                                               ".vgpr_count:"):
                     res[name][t[0][1:-1]] = int(t[1])
     return res
 
@@ -280,17 +281,36 @@ def test_step_kernels_fit_eight_waves_without_scratch(tmp_path):
 
 @pytest.mark.skipif(not os.path.exists(f"{LLVM_BIN}/llvm-readelf"), reason="ROCm LLVM tools absent")
 def test_rows_step_kernels_have_no_scratch(tmp_path):
-    """k_step_rows (four envs per wavefront, csrc/mdl_step_rows.hpp): one instantiation per tracker mode
-    and robot specialisation (A == 5, A <= 8), four package chunks; no spill to scratch, the A == 5
-    form within 104 VGPRs (5 waves per SIMD, the occupancy profiles/r05/rows_ab.txt was measured at),
-    the A <= 8 form within 128 (4 waves)."""
+    """k_step_rows (four envs per wavefront, csrc/mdl_step_rows.hpp): one instantiation per tracker mode,
+    robot specialisation (A == 5, A <= 8) and full-chunk count (NFULL 0 or 3), four package chunks; no
+    spill to scratch; config 4's form (stale tracker, A == 5, NFULL 3) within 72 VGPRs (7 waves per
+    SIMD, the occupancy profiles/r06/ab10 was measured at), the other A == 5 forms within 104, the
+    A <= 8 forms within 128 (4 waves); no SGPR spill in the A == 5 forms."""
     from marl_gpu import _lib
     res = _kernel_resources(_lib.LIB_PATH, tmp_path)
     rows = [n for n in res if "k_step_rows" in n]
-    assert len(rows) == 4, rows
+    assert len(rows) == 8, rows
     for n in rows:
         assert res[n]["private_segment_fixed_size"] == 0, (n, res[n])
-        assert res[n]["vgpr_count"] <= (104 if "ILi5ELi4E" in n else 128), (n, res[n])
+        cap = 72 if "k_step_rowsILb1ELi5ELi4ELi3E" in n else 104 if "ILi5ELi4E" in n else 128
+        assert res[n]["vgpr_count"] <= cap, (n, res[n])
+        if "ILi5ELi4E" in n:   # the A == 5 forms (configs 4 and 2 at >= 7,168 envs): no SGPR spill
+            assert res[n].get("sgpr_spill_count", 0) == 0, (n, res[n])
+
+
+@pytest.mark.skipif(not os.path.exists(f"{LLVM_BIN}/llvm-readelf"), reason="ROCm LLVM tools absent")
+def test_halves_step_kernels_have_no_scratch(tmp_path):
+    """k_step_halves (two envs per wavefront, csrc/mdl_step_halves.hpp): one instantiation per tracker
+    mode and full-chunk count (NFULL 0 or 3); no spill to scratch or SGPR spill; config 5's form (stale
+    tracker, NFULL 3) within 72 VGPRs (7 waves per SIMD, profiles/r06/ab9), the others within 80."""
+    from marl_gpu import _lib
+    res = _kernel_resources(_lib.LIB_PATH, tmp_path)
+    halves = [n for n in res if "k_step_halves" in n]
+    assert len(halves) == 4, halves
+    for n in halves:
+        assert res[n]["private_segment_fixed_size"] == 0, (n, res[n])
+        assert res[n].get("sgpr_spill_count", 0) == 0, (n, res[n])
+        assert res[n]["vgpr_count"] <= (72 if "k_step_halvesILb1ELi3E" in n else 80), (n, res[n])
 
 
 def test_bench_step_layout_flag():
